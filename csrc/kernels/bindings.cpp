@@ -1,0 +1,178 @@
+// pybind11 entry points for the HIP kernel library (module fleetx_amd._C._kernels).
+// Tensors cross the boundary as raw device addresses (uintptr_t) plus the
+// current HIP stream handle; shape checks live in fleetx_amd/ops/*.py.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <stdint.h>
+#include <vector>
+
+namespace py = pybind11;
+typedef uintptr_t ptr;
+
+extern "C" {
+int fx_coltile_splits(int rows, int cols);
+void fx_add_ln_fwd(int, const void*, const void*, const void*, const void*, const void*, void*,
+                   void*, float*, float*, int, int, float, float, uint64_t, hipStream_t);
+void fx_ln_bwd_row(int, const void*, const void*, const float*, const float*, const void*,
+                   const void*, void*, void*, int, int, float, uint64_t, hipStream_t);
+void fx_coltile_partial(int, int, const void*, const void*, const float*, const float*, float*,
+                        float*, int, int, int, hipStream_t);
+void fx_coltile_finalize(int, const float*, int, int, float*, void*, int, hipStream_t);
+void fx_bias_gelu_fwd(int, int, const void*, const void*, void*, long, int, hipStream_t);
+void fx_bias_gelu_bwd(int, int, const void*, const void*, const void*, void*, float*, int, int, int,
+                      hipStream_t);
+void fx_bias_dropout_add_fwd(int, const void*, const void*, const void*, void*, long, int, float,
+                             uint64_t, hipStream_t);
+void fx_dropout_bwd_colsum(int, const void*, void*, float*, int, int, int, float, uint64_t,
+                           hipStream_t);
+void fx_dropout_fwd(int, const void*, void*, long, float, uint64_t, hipStream_t);
+void fx_ce_stats(int, const void*, const int64_t*, int, int, long, float*, float*, float*, int,
+                 hipStream_t);
+void fx_ce_bwd(int, const void*, void*, const int64_t*, const float*, const float*, int, int, long,
+               int, hipStream_t);
+int fx_sumsq_blocks(long n);
+void fx_sumsq_f32(const float*, long, float*, int, hipStream_t);
+void fx_adamw_flat(int, float*, const float*, float*, float*, void*, long, float, float, float,
+                   float, float, float, float, const float*, const int*, hipStream_t);
+void fx_cast_f32(int, const float*, void*, long, hipStream_t);
+void fx_accum_f32(int, float*, const void*, long, int, hipStream_t);
+void fx_embedding_fwd(int, const int64_t*, const int64_t*, const void*, const void*, void*, int,
+                      int, long, long, hipStream_t);
+void fx_embedding_bwd(int, const int64_t*, const void*, float*, int, int, long, long,
+                      hipStream_t);
+int fx_flash_fwd(const void*, const void*, const void*, void*, float*, const long*, const long*,
+                 const long*, const long*, const int*, int, int, int, int, int, int, float, float,
+                 uint64_t, hipStream_t);
+int fx_flash_bwd(const void*, const void*, const void*, const void*, const void*, const float*,
+                 float*, void*, void*, void*, const long*, const long*, const long*, const long*,
+                 const long*, const long*, const int*, int, int, int, int, int, int, float, float,
+                 uint64_t, hipStream_t);
+int fx_fake_quant_fwd(int, const void*, void*, const float*, int, long, hipStream_t);
+void fx_absmax(int, const void*, long, float*, hipStream_t);
+int fx_decode_attn(const void*, const void*, const void*, void*, const int*, int, int, int, int,
+                   int, long, long, long, long, long, long, float, hipStream_t);
+}
+
+#define P(x) reinterpret_cast<void*>(x)
+#define CP(x) reinterpret_cast<const void*>(x)
+#define S(x) reinterpret_cast<hipStream_t>(x)
+#define F(x) reinterpret_cast<float*>(x)
+
+static std::vector<long> v3(const std::vector<long>& a) {
+  std::vector<long> r(a);
+  r.resize(3, 0);
+  return r;
+}
+
+PYBIND11_MODULE(_kernels, m) {
+  m.doc() = "FleetX-AMD HIP kernels (gfx950)";
+  m.def("coltile_splits", &fx_coltile_splits);
+  m.def("add_ln_fwd", [](int dt, ptr x, ptr bias, ptr res, ptr g, ptr b, ptr s_out, ptr y,
+                         ptr mean, ptr rstd, int rows, int h, float eps, float p, uint64_t key,
+                         ptr st) {
+    fx_add_ln_fwd(dt, CP(x), CP(bias), CP(res), CP(g), CP(b), P(s_out), P(y), F(mean), F(rstd),
+                  rows, h, eps, p, key, S(st));
+  });
+  m.def("ln_bwd_row", [](int dt, ptr dy, ptr s, ptr mean, ptr rstd, ptr g, ptr ds_in, ptr ds_out,
+                         ptr dx_out, int rows, int h, float p, uint64_t key, ptr st) {
+    fx_ln_bwd_row(dt, CP(dy), CP(s), F(mean), F(rstd), CP(g), CP(ds_in), P(ds_out), P(dx_out),
+                  rows, h, p, key, S(st));
+  });
+  m.def("coltile_partial", [](int dt, int mode, ptr a, ptr b, ptr mean, ptr rstd, ptr p0, ptr p1,
+                              int rows, int cols, int splits, ptr st) {
+    fx_coltile_partial(dt, mode, CP(a), CP(b), F(mean), F(rstd), F(p0), F(p1), rows, cols, splits,
+                       S(st));
+  });
+  m.def("coltile_finalize", [](int dt, ptr part, int splits, int cols, ptr out_f32, ptr out_t,
+                               int accumulate, ptr st) {
+    fx_coltile_finalize(dt, F(part), splits, cols, F(out_f32), P(out_t), accumulate, S(st));
+  });
+  m.def("bias_gelu_fwd", [](int dt, int erf, ptr x, ptr bias, ptr y, long n, int cols, ptr st) {
+    fx_bias_gelu_fwd(dt, erf, CP(x), CP(bias), P(y), n, cols, S(st));
+  });
+  m.def("bias_gelu_bwd", [](int dt, int erf, ptr dy, ptr x, ptr bias, ptr dx, ptr part, int rows,
+                            int cols, int splits, ptr st) {
+    fx_bias_gelu_bwd(dt, erf, CP(dy), CP(x), CP(bias), P(dx), F(part), rows, cols, splits, S(st));
+  });
+  m.def("bias_dropout_add_fwd", [](int dt, ptr x, ptr bias, ptr res, ptr out, long n, int cols,
+                                   float p, uint64_t key, ptr st) {
+    fx_bias_dropout_add_fwd(dt, CP(x), CP(bias), CP(res), P(out), n, cols, p, key, S(st));
+  });
+  m.def("dropout_bwd_colsum", [](int dt, ptr dout, ptr dx, ptr part, int rows, int cols,
+                                 int splits, float p, uint64_t key, ptr st) {
+    fx_dropout_bwd_colsum(dt, CP(dout), P(dx), F(part), rows, cols, splits, p, key, S(st));
+  });
+  m.def("dropout_fwd", [](int dt, ptr x, ptr y, long n, float p, uint64_t key, ptr st) {
+    fx_dropout_fwd(dt, CP(x), P(y), n, p, key, S(st));
+  });
+  m.def("ce_stats", [](int dt, ptr logits, ptr labels, int rows, int V, long vstart, ptr mx,
+                       ptr sm, ptr tg, int ignore, ptr st) {
+    fx_ce_stats(dt, CP(logits), reinterpret_cast<const int64_t*>(labels), rows, V, vstart, F(mx),
+                F(sm), F(tg), ignore, S(st));
+  });
+  m.def("ce_bwd", [](int dt, ptr logits, ptr dx, ptr labels, ptr lse, ptr g, int rows, int V,
+                     long vstart, int ignore, ptr st) {
+    fx_ce_bwd(dt, CP(logits), P(dx), reinterpret_cast<const int64_t*>(labels), F(lse), F(g), rows,
+              V, vstart, ignore, S(st));
+  });
+  m.def("sumsq_blocks", &fx_sumsq_blocks);
+  m.def("sumsq_f32", [](ptr x, long n, ptr partial, int blocks, ptr st) {
+    fx_sumsq_f32(F(x), n, F(partial), blocks, S(st));
+  });
+  m.def("adamw_flat", [](int dt, ptr p, ptr g, ptr mm, ptr vv, ptr p16, long n, float lr,
+                         float b1, float b2, float eps, float wd, float bc1, float bc2, ptr gscale,
+                         ptr skip, ptr st) {
+    fx_adamw_flat(dt, F(p), F(g), F(mm), F(vv), P(p16), n, lr, b1, b2, eps, wd, bc1, bc2,
+                  F(gscale), reinterpret_cast<const int*>(skip), S(st));
+  });
+  m.def("cast_f32", [](int dt, ptr x, ptr y, long n, ptr st) {
+    fx_cast_f32(dt, F(x), P(y), n, S(st));
+  });
+  m.def("accum_f32", [](int dt, ptr acc, ptr x, long n, int overwrite, ptr st) {
+    fx_accum_f32(dt, F(acc), CP(x), n, overwrite, S(st));
+  });
+  m.def("embedding_fwd", [](int dt, ptr ids, ptr pos, ptr W, ptr Pw, ptr out, int ntok, int h,
+                            long vstart, long vsize, ptr st) {
+    fx_embedding_fwd(dt, reinterpret_cast<const int64_t*>(ids),
+                     reinterpret_cast<const int64_t*>(pos), CP(W), CP(Pw), P(out), ntok, h, vstart,
+                     vsize, S(st));
+  });
+  m.def("embedding_bwd", [](int dt, ptr ids, ptr dout, ptr dW, int ntok, int h, long vstart,
+                            long vsize, ptr st) {
+    fx_embedding_bwd(dt, reinterpret_cast<const int64_t*>(ids), CP(dout), F(dW), ntok, h, vstart,
+                     vsize, S(st));
+  });
+  m.def("flash_fwd", [](ptr q, ptr k, ptr v, ptr out, ptr lse, std::vector<long> qs,
+                        std::vector<long> ks, std::vector<long> vs, std::vector<long> os,
+                        ptr kv_lens, int B, int H, int Sq, int Sk, int D, int causal, float scale,
+                        float p, uint64_t key, ptr st) {
+    auto a = v3(qs), b = v3(ks), c = v3(vs), d = v3(os);
+    return fx_flash_fwd(CP(q), CP(k), CP(v), P(out), F(lse), a.data(), b.data(), c.data(),
+                        d.data(), reinterpret_cast<const int*>(kv_lens), B, H, Sq, Sk, D, causal,
+                        scale, p, key, S(st));
+  });
+  m.def("flash_bwd", [](ptr q, ptr k, ptr v, ptr o, ptr dout, ptr lse, ptr delta, ptr dq, ptr dk,
+                        ptr dv, std::vector<long> qs, std::vector<long> ks, std::vector<long> vs,
+                        std::vector<long> os, std::vector<long> dqs, std::vector<long> dks,
+                        ptr kv_lens, int B, int H, int Sq, int Sk, int D, int causal, float scale,
+                        float p, uint64_t key, ptr st) {
+    auto a = v3(qs), b = v3(ks), c = v3(vs), d = v3(os), e = v3(dks), f = v3(dqs);
+    return fx_flash_bwd(CP(q), CP(k), CP(v), CP(o), CP(dout), F(lse), F(delta), P(dq), P(dk),
+                        P(dv), a.data(), b.data(), c.data(), d.data(), f.data(), e.data(),
+                        reinterpret_cast<const int*>(kv_lens), B, H, Sq, Sk, D, causal, scale, p,
+                        key, S(st));
+  });
+  m.def("fake_quant_fwd", [](int dt, ptr x, ptr y, ptr scale, int bits, long n, ptr st) {
+    return fx_fake_quant_fwd(dt, CP(x), P(y), F(scale), bits, n, S(st));
+  });
+  m.def("absmax", [](int dt, ptr x, long n, ptr out, ptr st) {
+    fx_absmax(dt, CP(x), n, F(out), S(st));
+  });
+  m.def("decode_attn", [](ptr q, ptr kc, ptr vc, ptr out, ptr lens, int B, int H, int D,
+                          int maxlen, int nsplit, long sqb, long sqh, long skb, long sks, long skh,
+                          long sob, float scale, ptr st) {
+    return fx_decode_attn(CP(q), CP(kc), CP(vc), P(out), reinterpret_cast<const int*>(lens), B, H,
+                          D, maxlen, nsplit, sqb, sqh, skb, sks, skh, sob, scale, S(st));
+  });
+}

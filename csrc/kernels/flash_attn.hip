@@ -1,0 +1,663 @@
+// Fused (flash-style) multi-head attention for gfx950: forward, and backward
+// as two atomic-free passes (dK/dV with keys on the MFMA lane, dQ with
+// queries on the lane).  Causal and key-padding masks, in-kernel dropout on
+// the attention probabilities from the counter hash of parallel/rng.py.
+//
+// Parity: replaces reference K03-K06 (matmul(q,k^T)*d^-1/2 ->
+// softmax_mask_fuse_upper_triangle -> dropout(local_seed) -> matmul(.,v) ->
+// head merge); `single_model.py:189-213`,
+// `hybrid_model.py:268-298`.  The [b, a, s, s] score tensor is never
+// materialised.
+//
+// CDNA4 structure (see docs/KERNELS.md):
+//  * MFMA v_mfma_f32_32x32x16_bf16, wave64.  Forward computes S^T = K.Q^T so
+//    each lane owns ONE query column: the row max / sum are in-lane plus one
+//    lane^32 exchange, and the S^T accumulator is directly the B operand of
+//    O^T = V^T.P^T (no LDS round trip for P).
+//  * V^T fragments come from ds_read_b64_tr_b16 (hardware transpose).
+//  * K/V tiles are XOR-swizzled in LDS (conflict-free for both the b128 row
+//    reads and the tr_b16 reads; verified by tools/lds_bank_sim.py).
+//  * K/V tiles go HBM -> LDS by global_load_lds (no VGPR staging, no
+//    ds_write pass); tile i+1 is in flight into the second LDS buffer while
+//    tile i computes, one vmcnt drain + barrier per tile.
+//  * blockIdx is remapped so the q-blocks of one (batch, head) run on one XCD
+//    (shared K/V stay in that XCD's L2); causal heavy blocks go first.
+#include "fx_common.h"
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+#define LDSV4(p) ((__attribute__((address_space(3))) v4s*)(p))
+
+namespace {
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+template <int D>
+__device__ __forceinline__ int swz(int row) {
+  if constexpr (D == 128) return ((row & 3) << 2) | ((row >> 2) & 3);
+  else return ((row >> 1) & 1) | (((row >> 2) & 1) << 1) | ((((row >> 1) ^ (row >> 3)) & 1) << 2);
+}
+// byte offset of 16-byte chunk `ch` of `row` in a [rows][D] 16-bit tile image
+template <int D>
+__device__ __forceinline__ int loff(int row, int ch) {
+  return row * (D * 2) + ((ch ^ swz<D>(row)) << 4);
+}
+
+// A/B fragment row read (32x32x16 operand): row r, k-step s, lane half h
+template <int D>
+__device__ __forceinline__ bf16x8 row_frag(const char* tile, int row, int s, int h) {
+  return *reinterpret_cast<const bf16x8*>(tile + loff<D>(row, 2 * s + h));
+}
+
+// Transposed fragment: lane gets column (dt*32 + (lane&31)) of rows
+// keybase+{0..3} and keybase+8+{0..3}; keybase includes 4*h.
+template <int D>
+__device__ __forceinline__ bf16x8 tr_frag(const char* tile, int keybase, int dt, int lane) {
+  const int gi = (lane >> 4) & 1, i = lane & 15, q = i >> 2, p = i & 3;
+  const int ch = dt * 4 + 2 * gi + (p >> 1);
+  const int b0 = loff<D>(keybase + q, ch) + 8 * (p & 1);
+  const int b1 = loff<D>(keybase + 8 + q, ch) + 8 * (p & 1);
+  v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDSV4(tile + b0));
+  v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDSV4(tile + b1));
+  short8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+__device__ __forceinline__ floatx16 mfma(const bf16x8& a, const bf16x8& b, const floatx16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// row index (within a 32-row C tile) held in register i for lane half h
+__device__ __forceinline__ int crow(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+// Tile loader: ROWS x D 16-bit elements straight into the swizzled LDS image
+// with global_load_lds (16 B per lane, 1 KiB per wave-instruction).  The LDS
+// side is lane-linear, so the XOR swizzle is applied to the per-lane GLOBAL
+// source address (rule: swizzle both sides or neither).  Rows past `nvalid`
+// are clamped to the last valid row; the kernels mask them.
+template <int D, int ROWS>
+struct Glds {
+  static constexpr int RB = D * 2;
+  static constexpr int NI = ROWS * RB / 1024 / 4;  // instructions per wave (4 waves)
+  static __device__ __forceinline__ void load(const uint16_t* base, long stride, int row0,
+                                              int nvalid, char* tile, int w, int lane) {
+    const int last = nvalid - 1;
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int blk = (w * NI + u) * 1024;
+      const int lin = blk + lane * 16;
+      const int row = lin / RB, chp = (lin % RB) >> 4;
+      const int chl = chp ^ swz<D>(row);
+      int grow = row0 + row;
+      grow = grow > last ? last : grow;
+      const uint16_t* src = base + (long)grow * stride + chl * 8;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(tile + blk), 16,
+                                       0, 0);
+    }
+  }
+};
+
+__device__ __forceinline__ void glds_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+struct AttnParams {
+  const uint16_t *q, *k, *v, *o, *dout;
+  uint16_t *out, *dq, *dk, *dv;
+  float *lse, *delta;
+  const int* kv_lens;
+  long sq_b, sq_s, sq_h;   // q strides (elements) batch / seq / head
+  long sk_b, sk_s, sk_h;   // k (and v) strides
+  long sv_b, sv_s, sv_h;
+  long so_b, so_s, so_h;   // out / dout strides (same layout)
+  long sdq_b, sdq_s, sdq_h;  // dq strides
+  long sdk_b, sdk_s, sdk_h;  // dk / dv strides
+  int B, H, Sq, Sk;
+  float scale;
+  uint32_t klo, khi, thr;
+  float drop_scale;
+};
+
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  const int xcd = bid & 7, pos = bid >> 3, q = nblk >> 3, r = nblk & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+}
+
+// ============================================================================
+// forward: WG = 4 waves x 32 queries = 128 queries; KV tile = 64 keys
+// ============================================================================
+template <int D, bool CAUSAL, bool DROP>
+__global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KV = 64, TB = KV * D * 2;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  const int nq = (P.Sq + 127) / 128;
+  const int nblk = nq * P.B * P.H;
+  const int lid = xcd_remap(blockIdx.x, nblk);
+  const int bh = lid / nq;
+  const int qblock = CAUSAL ? (nq - 1 - lid % nq) : (lid % nq);
+  const int b = bh / P.H, hd = bh % P.H;
+
+  const uint16_t* qp = P.q + b * P.sq_b + hd * P.sq_h;
+  const uint16_t* kp = P.k + b * P.sk_b + hd * P.sk_h;
+  const uint16_t* vp = P.v + b * P.sv_b + hd * P.sv_h;
+  int kv_len = P.Sk;
+  if (P.kv_lens) kv_len = min(kv_len, P.kv_lens[b]);
+
+  const int wq0 = qblock * 128 + w * 32;
+  const int qi = wq0 + (lane & 31);
+  bf16x8 qf[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    if (qi < P.Sq)
+      qf[s] = *reinterpret_cast<const bf16x8*>(qp + (long)qi * P.sq_s + 16 * s + 8 * h);
+    else
+      qf[s] = __builtin_bit_cast(bf16x8, (short8){0, 0, 0, 0, 0, 0, 0, 0});
+  }
+
+  int kv_end = kv_len;
+  if (CAUSAL) kv_end = min(kv_end, (qblock + 1) * 128);
+  const int ntiles = (kv_end + KV - 1) / KV;
+
+  floatx16 oacc[D / 32];
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) oacc[dt][i] = 0.f;
+  float m_run = -INFINITY, lsum = 0.f;
+  const float sl2 = P.scale * LOG2E;
+  const uint32_t cb = DROP ? (lowbias32((uint32_t)bh ^ P.khi) ^ P.klo) : 0u;
+
+  if (ntiles > 0) {
+    Glds<D, KV>::load(kp, P.sk_s, 0, kv_end, smem, w, lane);
+    Glds<D, KV>::load(vp, P.sv_s, 0, kv_end, smem + 2 * TB, w, lane);
+  }
+  glds_wait();
+  __syncthreads();
+
+  for (int it = 0; it < ntiles; ++it) {
+    const int cur = it & 1;
+    const char* kt = smem + cur * TB;
+    const char* vt = smem + 2 * TB + cur * TB;
+    const bool more = it + 1 < ntiles;
+    if (more) {
+      Glds<D, KV>::load(kp, P.sk_s, (it + 1) * KV, kv_end, smem + (cur ^ 1) * TB, w, lane);
+      Glds<D, KV>::load(vp, P.sv_s, (it + 1) * KV, kv_end, smem + 2 * TB + (cur ^ 1) * TB, w,
+                        lane);
+    }
+    const int kb = it * KV;
+    if (!(CAUSAL && kb > wq0 + 31)) {
+      floatx16 sacc[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[t][i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s)
+          sacc[t] = mfma(row_frag<D>(kt, 32 * t + (lane & 31), s, h), qf[s], sacc[t]);
+      }
+      const bool need_mask = (CAUSAL && kb + KV - 1 > wq0) || (kb + KV > kv_len);
+      float mloc = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float x = sacc[t][i] * sl2;
+          if (need_mask) {
+            const int key = kb + 32 * t + crow(i, h);
+            if ((CAUSAL && key > qi) || key >= kv_len) x = -INFINITY;
+          }
+          sacc[t][i] = x;
+          mloc = fmaxf(mloc, x);
+        }
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      const float m_new = fmaxf(m_run, mloc);
+      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+      const float alpha = exp2f(m_run - m_use);
+      m_run = m_new;
+      lsum *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+          float p0 = exp2f(sacc[t][i] - m_use), p1 = exp2f(sacc[t][i + 1] - m_use);
+          lsum += p0 + p1;
+          if (DROP) {
+            const int key = kb + 32 * t + crow(i, h);  // even
+            const uint32_t hh = lowbias32((((uint32_t)qi) << 16 | ((uint32_t)key >> 1)) ^ cb);
+            p0 = ((hh & 0xffffu) >= P.thr) ? p0 * P.drop_scale : 0.f;
+            p1 = ((hh >> 16) >= P.thr) ? p1 * P.drop_scale : 0.f;
+          }
+          sacc[t][i] = p0;
+          sacc[t][i + 1] = p1;
+        }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          bf16x8 pf;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pf[j] = (__bf16)sacc[t][8 * ss + j];
+          const int keybase = 32 * t + 16 * ss + 4 * h;
+#pragma unroll
+          for (int dt = 0; dt < D / 32; ++dt)
+            oacc[dt] = mfma(tr_frag<D>(vt, keybase, dt, lane), pf, oacc[dt]);
+        }
+    }
+    glds_wait();
+    __syncthreads();
+  }
+
+  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
+  if (qi < P.Sq) {
+    uint16_t* op = P.out + b * P.so_b + hd * P.so_h + (long)qi * P.so_s;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        ushort4 o;
+        o.x = float_to_bf16_bits(oacc[dt][4 * g + 0] * inv);
+        o.y = float_to_bf16_bits(oacc[dt][4 * g + 1] * inv);
+        o.z = float_to_bf16_bits(oacc[dt][4 * g + 2] * inv);
+        o.w = float_to_bf16_bits(oacc[dt][4 * g + 3] * inv);
+        *reinterpret_cast<ushort4*>(op + dt * 32 + 8 * g + 4 * h) = o;
+      }
+    if (h == 0) P.lse[(long)bh * P.Sq + qi] = ltot > 0.f ? (m_run + log2f(ltot)) * LN2 : INFINITY;
+  }
+}
+
+// ============================================================================
+// backward preprocess: delta[bh, q] = sum_d dO * O
+// ============================================================================
+template <int D>
+__global__ __launch_bounds__(256) void fa_bwd_pre_kernel(AttnParams P) {
+  // 8 threads x 16B per row chunk of 64 elems; D/8 threads per row
+  constexpr int TPR = D / 8;
+  const long row = (long)blockIdx.x * (256 / TPR) + threadIdx.x / TPR;
+  const int c = (threadIdx.x % TPR) * 8;
+  const long total = (long)P.B * P.H * P.Sq;
+  float s = 0.f;
+  if (row < total) {
+    const int q = row % P.Sq;
+    const int bh = row / P.Sq;
+    const int b = bh / P.H, hd = bh % P.H;
+    const long off = b * P.so_b + hd * P.so_h + (long)q * P.so_s + c;
+    float a[8], g[8];
+    load8<bf16>(P.o + off, a);
+    load8<bf16>(P.dout + off, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += a[j] * g[j];
+  }
+#pragma unroll
+  for (int o = TPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (row < total && (threadIdx.x % TPR) == 0) P.delta[row] = s;
+}
+
+// ============================================================================
+// backward dQ: WG = 4 waves x 32 queries; loop over 64-key tiles.
+//   S^T = K.Q^T, dP^T = V.dO^T (queries on lanes), dQ^T += K^T.dS^T
+// ============================================================================
+template <int D, bool CAUSAL, bool DROP>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KV = 64, TB = KV * D * 2;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  const int nq = (P.Sq + 127) / 128;
+  const int nblk = nq * P.B * P.H;
+  const int lid = xcd_remap(blockIdx.x, nblk);
+  const int bh = lid / nq;
+  const int qblock = CAUSAL ? (nq - 1 - lid % nq) : (lid % nq);
+  const int b = bh / P.H, hd = bh % P.H;
+  const uint16_t* qp = P.q + b * P.sq_b + hd * P.sq_h;
+  const uint16_t* kp = P.k + b * P.sk_b + hd * P.sk_h;
+  const uint16_t* vp = P.v + b * P.sv_b + hd * P.sv_h;
+  const uint16_t* dop = P.dout + b * P.so_b + hd * P.so_h;
+  int kv_len = P.Sk;
+  if (P.kv_lens) kv_len = min(kv_len, P.kv_lens[b]);
+
+  const int wq0 = qblock * 128 + w * 32;
+  const int qi = wq0 + (lane & 31);
+  const bool qvalid = qi < P.Sq;
+  bf16x8 qf[D / 16], gf[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    if (qvalid) {
+      qf[s] = *reinterpret_cast<const bf16x8*>(qp + (long)qi * P.sq_s + 16 * s + 8 * h);
+      gf[s] = *reinterpret_cast<const bf16x8*>(dop + (long)qi * P.so_s + 16 * s + 8 * h);
+    } else {
+      qf[s] = __builtin_bit_cast(bf16x8, (short8){0, 0, 0, 0, 0, 0, 0, 0});
+      gf[s] = qf[s];
+    }
+  }
+  const float lse2 = qvalid ? P.lse[(long)bh * P.Sq + qi] * LOG2E : INFINITY;
+  const float dlt = qvalid ? P.delta[(long)bh * P.Sq + qi] : 0.f;
+  const float sl2 = P.scale * LOG2E;
+  const uint32_t cb = DROP ? (lowbias32((uint32_t)bh ^ P.khi) ^ P.klo) : 0u;
+
+  int kv_end = kv_len;
+  if (CAUSAL) kv_end = min(kv_end, (qblock + 1) * 128);
+  const int ntiles = (kv_end + KV - 1) / KV;
+
+  floatx16 dqacc[D / 32];
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dqacc[dt][i] = 0.f;
+
+  if (ntiles > 0) {
+    Glds<D, KV>::load(kp, P.sk_s, 0, kv_end, smem, w, lane);
+    Glds<D, KV>::load(vp, P.sv_s, 0, kv_end, smem + 2 * TB, w, lane);
+  }
+  glds_wait();
+  __syncthreads();
+
+  for (int it = 0; it < ntiles; ++it) {
+    const int cur = it & 1;
+    const char* kt = smem + cur * TB;
+    const char* vt = smem + 2 * TB + cur * TB;
+    const bool more = it + 1 < ntiles;
+    if (more) {
+      Glds<D, KV>::load(kp, P.sk_s, (it + 1) * KV, kv_end, smem + (cur ^ 1) * TB, w, lane);
+      Glds<D, KV>::load(vp, P.sv_s, (it + 1) * KV, kv_end, smem + 2 * TB + (cur ^ 1) * TB, w,
+                        lane);
+    }
+    const int kb = it * KV;
+    if (!(CAUSAL && kb > wq0 + 31)) {
+      const bool need_mask = (CAUSAL && kb + KV - 1 > wq0) || (kb + KV > kv_len);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        floatx16 sacc, dpacc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[i] = dpacc[i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s) {
+          sacc = mfma(row_frag<D>(kt, 32 * t + (lane & 31), s, h), qf[s], sacc);
+          dpacc = mfma(row_frag<D>(vt, 32 * t + (lane & 31), s, h), gf[s], dpacc);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+          const int key = kb + 32 * t + crow(i, h);
+          float p0 = exp2f(sacc[i] * sl2 - lse2), p1 = exp2f(sacc[i + 1] * sl2 - lse2);
+          if (need_mask) {
+            if ((CAUSAL && key > qi) || key >= kv_len) p0 = 0.f;
+            if ((CAUSAL && key + 1 > qi) || key + 1 >= kv_len) p1 = 0.f;
+          }
+          float dp0 = dpacc[i], dp1 = dpacc[i + 1];
+          if (DROP) {
+            const uint32_t hh = lowbias32((((uint32_t)qi) << 16 | ((uint32_t)key >> 1)) ^ cb);
+            dp0 = ((hh & 0xffffu) >= P.thr) ? dp0 * P.drop_scale : 0.f;
+            dp1 = ((hh >> 16) >= P.thr) ? dp1 * P.drop_scale : 0.f;
+          }
+          sacc[i] = p0 * (dp0 - dlt);
+          sacc[i + 1] = p1 * (dp1 - dlt);
+        }
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          bf16x8 df;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) df[j] = (__bf16)sacc[8 * ss + j];
+          const int keybase = 32 * t + 16 * ss + 4 * h;
+#pragma unroll
+          for (int dt = 0; dt < D / 32; ++dt)
+            dqacc[dt] = mfma(tr_frag<D>(kt, keybase, dt, lane), df, dqacc[dt]);
+        }
+      }
+    }
+    glds_wait();
+    __syncthreads();
+  }
+  if (qvalid) {
+    uint16_t* dqp = P.dq + b * P.sdq_b + hd * P.sdq_h + (long)qi * P.sdq_s;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        ushort4 o;
+        o.x = float_to_bf16_bits(dqacc[dt][4 * g + 0] * P.scale);
+        o.y = float_to_bf16_bits(dqacc[dt][4 * g + 1] * P.scale);
+        o.z = float_to_bf16_bits(dqacc[dt][4 * g + 2] * P.scale);
+        o.w = float_to_bf16_bits(dqacc[dt][4 * g + 3] * P.scale);
+        *reinterpret_cast<ushort4*>(dqp + dt * 32 + 8 * g + 4 * h) = o;
+      }
+  }
+}
+
+// ============================================================================
+// backward dK/dV: WG = 4 waves x 32 keys = 128 keys; loop over 64-query tiles
+//   S = Q.K^T, dP = dO.V^T (keys on lanes, queries in registers)
+//   dV^T += dO^T.(P o Z),  dK^T += Q^T.dS
+// ============================================================================
+template <int D, bool CAUSAL, bool DROP>
+__global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnParams P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int QT = 64, TB = QT * D * 2;
+  // layout: [Q tile][dO tile][lse2 64 floats][delta 64 floats]
+  char* qt = smem;
+  char* gt = smem + TB;
+  float* lse_s = reinterpret_cast<float*>(smem + 2 * TB);
+  float* dl_s = lse_s + QT;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  const int nk = (P.Sk + 127) / 128;
+  const int nblk = nk * P.B * P.H;
+  const int lid = xcd_remap(blockIdx.x, nblk);
+  const int bh = lid / nk;
+  const int kblock = lid % nk;  // causal: low key blocks are the heavy ones
+  const int b = bh / P.H, hd = bh % P.H;
+  const uint16_t* qp = P.q + b * P.sq_b + hd * P.sq_h;
+  const uint16_t* kp = P.k + b * P.sk_b + hd * P.sk_h;
+  const uint16_t* vp = P.v + b * P.sv_b + hd * P.sv_h;
+  const uint16_t* dop = P.dout + b * P.so_b + hd * P.so_h;
+  int kv_len = P.Sk;
+  if (P.kv_lens) kv_len = min(kv_len, P.kv_lens[b]);
+
+  const int wk0 = kblock * 128 + w * 32;
+  const int ki = wk0 + (lane & 31);
+  const bool kvalid = ki < kv_len;
+  bf16x8 kf[D / 16], vf[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    if (ki < P.Sk) {
+      kf[s] = *reinterpret_cast<const bf16x8*>(kp + (long)ki * P.sk_s + 16 * s + 8 * h);
+      vf[s] = *reinterpret_cast<const bf16x8*>(vp + (long)ki * P.sv_s + 16 * s + 8 * h);
+    } else {
+      kf[s] = __builtin_bit_cast(bf16x8, (short8){0, 0, 0, 0, 0, 0, 0, 0});
+      vf[s] = kf[s];
+    }
+  }
+  floatx16 dkacc[D / 32], dvacc[D / 32];
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dkacc[dt][i] = dvacc[dt][i] = 0.f;
+  const float sl2 = P.scale * LOG2E;
+  const uint32_t cb = DROP ? (lowbias32((uint32_t)bh ^ P.khi) ^ P.klo) : 0u;
+
+  const int q_begin = CAUSAL ? (kblock * 128 / QT) * QT : 0;
+  for (int qb = q_begin; qb < P.Sq; qb += QT) {
+    __syncthreads();  // previous tile fully consumed
+    Glds<D, QT>::load(qp, P.sq_s, qb, P.Sq, qt, w, lane);
+    Glds<D, QT>::load(dop, P.so_s, qb, P.Sq, gt, w, lane);
+    if (tid < QT) {
+      const int q = qb + tid;
+      lse_s[tid] = q < P.Sq ? P.lse[(long)bh * P.Sq + q] * LOG2E : INFINITY;
+      dl_s[tid] = q < P.Sq ? P.delta[(long)bh * P.Sq + q] : 0.f;
+    }
+    glds_wait();
+    __syncthreads();
+    if (CAUSAL && qb + QT - 1 < wk0) continue;  // whole tile above this wave's keys
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int q0 = qb + 32 * t;
+      if (CAUSAL && q0 + 31 < wk0) continue;
+      floatx16 sacc, dpacc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[i] = dpacc[i] = 0.f;
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        sacc = mfma(row_frag<D>(qt, 32 * t + (lane & 31), s, h), kf[s], sacc);
+        dpacc = mfma(row_frag<D>(gt, 32 * t + (lane & 31), s, h), vf[s], dpacc);
+      }
+      floatx16 pd;  // dropped probabilities (for dV)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int ql_ = 32 * t + crow(i, h);
+        const int q = qb + ql_;
+        float p = exp2f(sacc[i] * sl2 - lse_s[ql_]);
+        if ((CAUSAL && ki > q) || !kvalid || q >= P.Sq) p = 0.f;
+        float z = 1.f;
+        if (DROP) {
+          const uint32_t hh = lowbias32((((uint32_t)q) << 16 | ((uint32_t)ki >> 1)) ^ cb);
+          const uint32_t r = (ki & 1) ? (hh >> 16) : (hh & 0xffffu);
+          z = r >= P.thr ? P.drop_scale : 0.f;
+        }
+        pd[i] = p * z;
+        sacc[i] = p * (dpacc[i] * z - dl_s[ql_]);  // dS
+      }
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        bf16x8 pf, df;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          pf[j] = (__bf16)pd[8 * ss + j];
+          df[j] = (__bf16)sacc[8 * ss + j];
+        }
+        const int qbase = 32 * t + 16 * ss + 4 * h;
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt) {
+          dvacc[dt] = mfma(tr_frag<D>(gt, qbase, dt, lane), pf, dvacc[dt]);
+          dkacc[dt] = mfma(tr_frag<D>(qt, qbase, dt, lane), df, dkacc[dt]);
+        }
+      }
+    }
+  }
+  if (ki < P.Sk) {
+    uint16_t* dkp = P.dk + b * P.sdk_b + hd * P.sdk_h + (long)ki * P.sdk_s;
+    uint16_t* dvp = P.dv + b * P.sdk_b + hd * P.sdk_h + (long)ki * P.sdk_s;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        ushort4 a, c;
+        a.x = float_to_bf16_bits(dkacc[dt][4 * g + 0] * P.scale);
+        a.y = float_to_bf16_bits(dkacc[dt][4 * g + 1] * P.scale);
+        a.z = float_to_bf16_bits(dkacc[dt][4 * g + 2] * P.scale);
+        a.w = float_to_bf16_bits(dkacc[dt][4 * g + 3] * P.scale);
+        c.x = float_to_bf16_bits(dvacc[dt][4 * g + 0]);
+        c.y = float_to_bf16_bits(dvacc[dt][4 * g + 1]);
+        c.z = float_to_bf16_bits(dvacc[dt][4 * g + 2]);
+        c.w = float_to_bf16_bits(dvacc[dt][4 * g + 3]);
+        *reinterpret_cast<ushort4*>(dkp + dt * 32 + 8 * g + 4 * h) = a;
+        *reinterpret_cast<ushort4*>(dvp + dt * 32 + 8 * g + 4 * h) = c;
+      }
+  }
+}
+
+AttnParams make_params(const void* q, const void* k, const void* v, const long* qs,
+                       const long* ks, const long* vs, int B, int H, int Sq, int Sk, float scale,
+                       float p, uint64_t key) {
+  AttnParams P{};
+  P.q = (const uint16_t*)q;
+  P.k = (const uint16_t*)k;
+  P.v = (const uint16_t*)v;
+  P.sq_b = qs[0]; P.sq_s = qs[1]; P.sq_h = qs[2];
+  P.sk_b = ks[0]; P.sk_s = ks[1]; P.sk_h = ks[2];
+  P.sv_b = vs[0]; P.sv_s = vs[1]; P.sv_h = vs[2];
+  P.B = B; P.H = H; P.Sq = Sq; P.Sk = Sk;
+  P.scale = scale;
+  P.klo = (uint32_t)(key & 0xffffffffu);
+  P.khi = (uint32_t)(key >> 32);
+  P.thr = (uint32_t)(p * 65536.0f + 0.5f);
+  P.drop_scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  return P;
+}
+
+template <template <int, bool, bool> class K>
+struct Dummy {};
+
+}  // namespace
+
+#define FA_DISPATCH(KERNEL, D, causal, drop, grid, smem, st, P)                         \
+  do {                                                                                  \
+    if (D == 128) {                                                                     \
+      if (causal) {                                                                     \
+        if (drop) KERNEL<128, true, true><<<grid, 256, smem, st>>>(P);                  \
+        else KERNEL<128, true, false><<<grid, 256, smem, st>>>(P);                      \
+      } else {                                                                          \
+        if (drop) KERNEL<128, false, true><<<grid, 256, smem, st>>>(P);                 \
+        else KERNEL<128, false, false><<<grid, 256, smem, st>>>(P);                     \
+      }                                                                                 \
+    } else {                                                                            \
+      if (causal) {                                                                     \
+        if (drop) KERNEL<64, true, true><<<grid, 256, smem, st>>>(P);                   \
+        else KERNEL<64, true, false><<<grid, 256, smem, st>>>(P);                       \
+      } else {                                                                          \
+        if (drop) KERNEL<64, false, true><<<grid, 256, smem, st>>>(P);                  \
+        else KERNEL<64, false, false><<<grid, 256, smem, st>>>(P);                      \
+      }                                                                                 \
+    }                                                                                   \
+  } while (0)
+
+// strides arrays are {batch, seq, head} in elements; head dim contiguous.
+extern "C" int fx_flash_fwd(const void* q, const void* k, const void* v, void* out, float* lse,
+                            const long* qs, const long* ks, const long* vs, const long* os,
+                            const int* kv_lens, int B, int H, int Sq, int Sk, int D, int causal,
+                            float scale, float p, uint64_t key, hipStream_t st) {
+  if (D != 64 && D != 128) return -1;
+  AttnParams P = make_params(q, k, v, qs, ks, vs, B, H, Sq, Sk, scale, p, key);
+  P.out = (uint16_t*)out;
+  P.lse = lse;
+  P.kv_lens = kv_lens;
+  P.so_b = os[0]; P.so_s = os[1]; P.so_h = os[2];
+  const int nq = (Sq + 127) / 128;
+  const int grid = nq * B * H;
+  const size_t smem = 4 * 64 * D * 2;
+  FA_DISPATCH(fa_fwd_kernel, D, causal, p > 0.f, grid, smem, st, P);
+  return 0;
+}
+
+// o/dout share strides `os`; dq uses `dqs`; dk/dv share `dks`.
+extern "C" int fx_flash_bwd(const void* q, const void* k, const void* v, const void* o,
+                            const void* dout, const float* lse, float* delta, void* dq, void* dk,
+                            void* dv, const long* qs, const long* ks, const long* vs,
+                            const long* os, const long* dqs, const long* dks, const int* kv_lens,
+                            int B, int H,
+                            int Sq, int Sk, int D, int causal, float scale, float p, uint64_t key,
+                            hipStream_t st) {
+  if (D != 64 && D != 128) return -1;
+  AttnParams P = make_params(q, k, v, qs, ks, vs, B, H, Sq, Sk, scale, p, key);
+  P.o = (const uint16_t*)o;
+  P.dout = (const uint16_t*)dout;
+  P.lse = const_cast<float*>(lse);
+  P.delta = delta;
+  P.dq = (uint16_t*)dq;
+  P.dk = (uint16_t*)dk;
+  P.dv = (uint16_t*)dv;
+  P.kv_lens = kv_lens;
+  P.so_b = os[0]; P.so_s = os[1]; P.so_h = os[2];
+  P.sdk_b = dks[0]; P.sdk_s = dks[1]; P.sdk_h = dks[2];
+  P.sdq_b = dqs[0]; P.sdq_s = dqs[1]; P.sdq_h = dqs[2];
+  {
+    const long rows = (long)B * H * Sq;
+    const int rpb = 256 / (D / 8);
+    const int grid = (int)((rows + rpb - 1) / rpb);
+    if (D == 128) fa_bwd_pre_kernel<128><<<grid, 256, 0, st>>>(P);
+    else fa_bwd_pre_kernel<64><<<grid, 256, 0, st>>>(P);
+  }
+  {
+    const int nq = (Sq + 127) / 128;
+    const size_t smem = 4 * 64 * D * 2;
+    FA_DISPATCH(fa_bwd_dq_kernel, D, causal, p > 0.f, nq * B * H, smem, st, P);
+  }
+  {
+    const int nk = (Sk + 127) / 128;
+    const size_t smem = 2 * 64 * D * 2 + 2 * 64 * 4;
+    FA_DISPATCH(fa_bwd_dkdv_kernel, D, causal, p > 0.f, nk * B * H, smem, st, P);
+  }
+  return 0;
+}

@@ -1,0 +1,333 @@
+// Softmax cross-entropy (vocab-parallel capable), fused AdamW over flat fp32
+// buffers, squared-norm partials, and the (vocab-parallel) embedding.
+//
+// Parity: reference K10 (VocabParallelEmbedding / nn.Embedding), K11
+// (ParallelCrossEntropy / CrossEntropyLoss kept in fp32), K12-K14 (multi-
+// precision AdamW, ClipGradByGlobalNorm, GradScaler) -- SURVEY.md §2.10.
+//
+// MI355X design notes:
+//  * CE: one 256-thread workgroup per token row, online (max, sum-exp) in fp32
+//    over 16-byte vector loads; logits never up-cast in memory.  The backward
+//    overwrites the logits buffer in place with dlogits (saves V x tokens x 2B).
+//    Vocab-parallel statistics are combined by two tiny RCCL all-reduces on
+//    the host side (max, then [sum, target]).
+//  * AdamW: the optimizer owns flat fp32 master/grad/m/v buffers (tensor
+//    fusion, reference P09), so an update is ONE launch per parameter group;
+//    the clip coefficient and found-inf flag are read from device memory, so
+//    the step never syncs the host.
+#include "fx_common.h"
+
+namespace {
+
+// --------------------------------------------------------------- CE stats
+template <typename T>
+__global__ __launch_bounds__(256) void ce_stats_kernel(
+    const uint16_t* __restrict__ logits, const int64_t* __restrict__ labels, int rows, int V,
+    long vocab_start, float* __restrict__ out_max, float* __restrict__ out_sum,
+    float* __restrict__ out_tgt, int ignore_index) {
+  const int row = blockIdx.x;
+  const uint16_t* x = logits + (size_t)row * V;
+  float m = -INFINITY, s = 0.f;
+  const int nv = V / 8;
+  for (int v = threadIdx.x; v < nv; v += 256) {
+    float a[8];
+    load8<T>(x + v * 8, a);
+    float lm = a[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) lm = fmaxf(lm, a[j]);
+    if (lm > m) {
+      s *= __expf(m - lm);
+      m = lm;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += __expf(a[j] - m);
+  }
+  for (int c = nv * 8 + threadIdx.x; c < V; c += 256) {
+    float a = Elt<T>::to_f(x[c]);
+    if (a > m) {
+      s *= __expf(m - a);
+      m = a;
+    }
+    s += __expf(a - m);
+  }
+  // block reduce (max, sum)
+  __shared__ float sm[4], ss[4];
+  float wm = wave_max(m);
+  float ws = wave_sum(m == -INFINITY ? 0.f : s * __expf(m - wm));
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+    sm[w] = wm;
+    ss[w] = ws;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+    float S = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) S += ss[k] * __expf(sm[k] - M);
+    out_max[row] = M;
+    out_sum[row] = S;
+    const long lab = labels[row];
+    const long local = lab - vocab_start;
+    float t = 0.f;
+    if (lab != ignore_index && local >= 0 && local < V) t = Elt<T>::to_f(x[local]);
+    out_tgt[row] = t;
+  }
+}
+
+// dlogits = (softmax - onehot) * g[row], written in place (or to dx).
+template <typename T>
+__global__ __launch_bounds__(256) void ce_bwd_kernel(const uint16_t* __restrict__ logits,
+                                                     uint16_t* __restrict__ dx,
+                                                     const int64_t* __restrict__ labels,
+                                                     const float* __restrict__ lse,
+                                                     const float* __restrict__ g, int V,
+                                                     long vocab_start, int ignore_index) {
+  const int row = blockIdx.x;
+  const uint16_t* x = logits + (size_t)row * V;
+  uint16_t* d = dx + (size_t)row * V;
+  const float L = lse[row];
+  const float gr = g[row];
+  const long lab = labels[row];
+  const long local = (lab == ignore_index) ? -1 : lab - vocab_start;
+  const int nv = V / 8;
+  for (int v = threadIdx.x; v < nv; v += 256) {
+    float a[8];
+    load8<T>(x + v * 8, a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float p = __expf(a[j] - L);
+      if (v * 8 + j == local) p -= 1.f;
+      a[j] = p * gr;
+    }
+    store8<T>(d + v * 8, a);
+  }
+  for (int c = nv * 8 + threadIdx.x; c < V; c += 256) {
+    float p = __expf(Elt<T>::to_f(x[c]) - L);
+    if (c == local) p -= 1.f;
+    d[c] = Elt<T>::from_f(p * gr);
+  }
+}
+
+// --------------------------------------------------------------- norms
+// partial[block] = sum of squares over a grid-stride slice (fp32 input)
+__global__ __launch_bounds__(256) void sumsq_f32_kernel(const float* __restrict__ x, long n,
+                                                        float* __restrict__ partial) {
+  float s = 0.f;
+  const long n4 = n / 4;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float4 v = x4[i];
+    s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  for (long i = n4 * 4 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    s += x[i] * x[i];
+  __shared__ float red[4];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// --------------------------------------------------------------- AdamW
+// p (fp32 master), g (fp32), m, v (fp32); optional 16-bit model copy.
+// gscale: device scalar multiplied into g (clip coef / unscale); skip: device
+// int flag (found inf) -> no update.
+template <typename T>
+__global__ __launch_bounds__(256) void adamw_flat_kernel(
+    float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+    float* __restrict__ v, uint16_t* __restrict__ p16, long n, float lr, float beta1,
+    float beta2, float eps, float wd, float bc1, float bc2, const float* __restrict__ gscale,
+    const int* __restrict__ skip) {
+  if (skip && *skip) return;
+  const float gs = gscale ? *gscale : 1.f;
+  const float step_size = lr / bc1;
+  const float inv_sqrt_bc2 = rsqrtf(bc2);
+  const long n4 = n / 4;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    float* pa = &pp.x;
+    float* ga = &gg.x;
+    float* ma = &mm.x;
+    float* va = &vv.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gr = ga[j] * gs;
+      ma[j] = beta1 * ma[j] + (1.f - beta1) * gr;
+      va[j] = beta2 * va[j] + (1.f - beta2) * gr * gr;
+      float denom = sqrtf(va[j]) * inv_sqrt_bc2 + eps;
+      pa[j] = pa[j] * (1.f - lr * wd) - step_size * ma[j] / denom;
+    }
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    if (p16) {
+      ushort4 o;
+      o.x = Elt<T>::from_f(pa[0]);
+      o.y = Elt<T>::from_f(pa[1]);
+      o.z = Elt<T>::from_f(pa[2]);
+      o.w = Elt<T>::from_f(pa[3]);
+      reinterpret_cast<ushort4*>(p16)[i] = o;
+    }
+  }
+  for (long i = n4 * 4 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    float gr = g[i] * gs;
+    m[i] = beta1 * m[i] + (1.f - beta1) * gr;
+    v[i] = beta2 * v[i] + (1.f - beta2) * gr * gr;
+    float denom = sqrtf(v[i]) * inv_sqrt_bc2 + eps;
+    p[i] = p[i] * (1.f - lr * wd) - step_size * m[i] / denom;
+    if (p16) p16[i] = Elt<T>::from_f(p[i]);
+  }
+}
+
+// copy fp32 -> 16-bit (param refresh after all-gather / load)
+template <typename T>
+__global__ __launch_bounds__(256) void cast_f32_kernel(const float* __restrict__ x,
+                                                       uint16_t* __restrict__ y, long n) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    y[i] = Elt<T>::from_f(x[i]);
+}
+
+// acc(fp32) += x (16-bit), used by grad-accumulation hooks
+template <typename T>
+__global__ __launch_bounds__(256) void accum_f32_kernel(float* __restrict__ acc,
+                                                        const uint16_t* __restrict__ x, long n,
+                                                        int overwrite) {
+  const long n8 = n / 8;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    float a[8];
+    load8<T>(x + i * 8, a);
+    float4* dst = reinterpret_cast<float4*>(acc + i * 8);
+    float4 d0 = overwrite ? make_float4(0, 0, 0, 0) : dst[0];
+    float4 d1 = overwrite ? make_float4(0, 0, 0, 0) : dst[1];
+    d0.x += a[0]; d0.y += a[1]; d0.z += a[2]; d0.w += a[3];
+    d1.x += a[4]; d1.y += a[5]; d1.z += a[6]; d1.w += a[7];
+    dst[0] = d0;
+    dst[1] = d1;
+  }
+  for (long i = n8 * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    acc[i] = (overwrite ? 0.f : acc[i]) + Elt<T>::to_f(x[i]);
+}
+
+// --------------------------------------------------------------- embedding
+// out[t] = (id in shard ? W[id - vstart] : 0) + (P ? P[pos[t]] : 0)
+template <typename T>
+__global__ __launch_bounds__(256) void embedding_fwd_kernel(
+    const int64_t* __restrict__ ids, const int64_t* __restrict__ pos,
+    const uint16_t* __restrict__ W, const uint16_t* __restrict__ P, uint16_t* __restrict__ out,
+    int ntok, int h, long vstart, long vsize) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= ntok) return;
+  const long id = ids[t] - vstart;
+  const bool in = id >= 0 && id < vsize;
+  const long pp = P ? pos[t] : 0;
+  for (int c = lane * 8; c < h; c += 512) {
+    float a[8];
+    if (in) load8<T>(W + (size_t)id * h + c, a);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = 0.f;
+    }
+    if (P) {
+      float b[8];
+      load8<T>(P + (size_t)pp * h + c, b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += b[j];
+    }
+    store8<T>(out + (size_t)t * h + c, a);
+  }
+}
+
+// dW[id - vstart] += dout[t] (fp32 atomics, 256 contiguous bytes per wave op)
+template <typename T>
+__global__ __launch_bounds__(256) void embedding_bwd_kernel(const int64_t* __restrict__ ids,
+                                                            const uint16_t* __restrict__ dout,
+                                                            float* __restrict__ dW, int ntok, int h,
+                                                            long vstart, long vsize) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= ntok) return;
+  const long id = ids[t] - vstart;
+  if (id < 0 || id >= vsize) return;
+  float* dst = dW + (size_t)id * h;
+  const uint16_t* src = dout + (size_t)t * h;
+  for (int c = lane; c < h; c += 64) atomicAdd(dst + c, Elt<T>::to_f(src[c]));
+}
+
+inline int grid_n(long n, int per = 256) {
+  long g = (n + per - 1) / per;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+#define FX_DISPATCH_T(dtype, ...) \
+  if (dtype == 0) {               \
+    using T = bf16;               \
+    __VA_ARGS__;                  \
+  } else {                        \
+    using T = f16;                \
+    __VA_ARGS__;                  \
+  }
+
+extern "C" void fx_ce_stats(int dtype, const void* logits, const int64_t* labels, int rows, int V,
+                            long vocab_start, float* out_max, float* out_sum, float* out_tgt,
+                            int ignore_index, hipStream_t st) {
+  FX_DISPATCH_T(dtype, ce_stats_kernel<T><<<rows, 256, 0, st>>>(
+                           (const uint16_t*)logits, labels, rows, V, vocab_start, out_max, out_sum,
+                           out_tgt, ignore_index));
+}
+
+extern "C" void fx_ce_bwd(int dtype, const void* logits, void* dx, const int64_t* labels,
+                          const float* lse, const float* g, int rows, int V, long vocab_start,
+                          int ignore_index, hipStream_t st) {
+  FX_DISPATCH_T(dtype, ce_bwd_kernel<T><<<rows, 256, 0, st>>>(
+                           (const uint16_t*)logits, (uint16_t*)dx, labels, lse, g, V, vocab_start,
+                           ignore_index));
+}
+
+extern "C" int fx_sumsq_blocks(long n) { return grid_n(n / 4 + 1, 256) > 1024 ? 1024 : grid_n(n / 4 + 1, 256); }
+
+extern "C" void fx_sumsq_f32(const float* x, long n, float* partial, int blocks, hipStream_t st) {
+  sumsq_f32_kernel<<<blocks, 256, 0, st>>>(x, n, partial);
+}
+
+extern "C" void fx_adamw_flat(int dtype, float* p, const float* g, float* m, float* v, void* p16,
+                              long n, float lr, float beta1, float beta2, float eps, float wd,
+                              float bc1, float bc2, const float* gscale, const int* skip,
+                              hipStream_t st) {
+  int grid = grid_n(n / 4 + 1, 256);
+  FX_DISPATCH_T(dtype, adamw_flat_kernel<T><<<grid, 256, 0, st>>>(
+                           p, g, m, v, (uint16_t*)p16, n, lr, beta1, beta2, eps, wd, bc1, bc2,
+                           gscale, skip));
+}
+
+extern "C" void fx_cast_f32(int dtype, const float* x, void* y, long n, hipStream_t st) {
+  FX_DISPATCH_T(dtype, cast_f32_kernel<T><<<grid_n(n), 256, 0, st>>>(x, (uint16_t*)y, n));
+}
+
+extern "C" void fx_accum_f32(int dtype, float* acc, const void* x, long n, int overwrite,
+                             hipStream_t st) {
+  FX_DISPATCH_T(dtype, accum_f32_kernel<T><<<grid_n(n / 8 + 1), 256, 0, st>>>(
+                           acc, (const uint16_t*)x, n, overwrite));
+}
+
+extern "C" void fx_embedding_fwd(int dtype, const int64_t* ids, const int64_t* pos, const void* W,
+                                 const void* P, void* out, int ntok, int h, long vstart,
+                                 long vsize, hipStream_t st) {
+  FX_DISPATCH_T(dtype, embedding_fwd_kernel<T><<<(ntok + 3) / 4, 256, 0, st>>>(
+                           ids, pos, (const uint16_t*)W, (const uint16_t*)P, (uint16_t*)out, ntok,
+                           h, vstart, vsize));
+}
+
+extern "C" void fx_embedding_bwd(int dtype, const int64_t* ids, const void* dout, float* dW,
+                                 int ntok, int h, long vstart, long vsize, hipStream_t st) {
+  FX_DISPATCH_T(dtype, embedding_bwd_kernel<T><<<(ntok + 3) / 4, 256, 0, st>>>(
+                           ids, (const uint16_t*)dout, dW, ntok, h, vstart, vsize));
+}

@@ -1,0 +1,678 @@
+// LayerNorm (+ fused residual/bias/dropout add), bias+GeLU, bias+dropout+add,
+// and the column-tile reduction kernels that produce dgamma/dbeta/dbias.
+//
+// Parity: reference K07 (nn.LayerNorm eps 1e-5/1e-6/1e-12), K08 (gelu tanh /
+// erf), K09 (residual dropout + add under upscale_in_train) -- SURVEY.md §2.10.
+//
+// MI355X design:
+//  * row kernels: one wave64 per row, 16-byte vector loads (8 x 16-bit) with
+//    lane-interleaved vectors so a wave instruction covers 1 KiB contiguous;
+//    the row is cached in VGPRs between the statistics pass and the
+//    normalisation pass (VPT template = vectors per lane);
+//  * column reductions (dgamma, dbeta, dbias) use a 128-column x 16-row
+//    tiling (256-byte row segments) with per-split fp32 partials and a tiny
+//    finalize kernel -- no float atomics, bitwise reproducible.
+#include "fx_common.h"
+
+namespace {
+
+struct DropCfg {
+  uint32_t klo, khi, thr;  // drop when rand16 < thr
+  float scale;             // 1/(1-p)
+  int enabled;
+};
+
+__device__ __forceinline__ float drop_apply(float v, uint64_t idx, const DropCfg& d) {
+  if (!d.enabled) return v;
+  uint32_t h = elem_rand_pair(idx, d.klo, d.khi);
+  uint32_t r = (idx & 1) ? (h >> 16) : (h & 0xffffu);
+  return r >= d.thr ? v * d.scale : 0.f;
+}
+
+// ---------------------------------------------------------------------------
+// Fused forward:  s = residual + dropout(x + bias);  y = LN(s) * g + b
+// Any of residual/bias may be null; dropout optional.  If s_out is null the
+// sum is not stored (plain LN when residual & bias are null and no dropout).
+// ---------------------------------------------------------------------------
+template <typename T, int VPT>
+__global__ __launch_bounds__(256) void add_ln_fwd_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ bias,
+    const uint16_t* __restrict__ residual, const uint16_t* __restrict__ gamma,
+    const uint16_t* __restrict__ beta, uint16_t* __restrict__ s_out,
+    uint16_t* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+    int rows, int h, float eps, DropCfg drop) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const size_t base = (size_t)row * h;
+  float v[VPT][8];
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = (i * 64 + lane) * 8;
+    load8<T>(x + base + c, v[i]);
+    if (bias) {
+      float b[8];
+      load8<T>(bias + c, b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] += b[j];
+    }
+    if (drop.enabled) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = drop_apply(v[i][j], base + c + j, drop);
+    }
+    if (residual) {
+      float r[8];
+      load8<T>(residual + base + c, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] += r[j];
+    }
+    if (s_out) {
+      store8<T>(s_out + base + c, v[i]);
+      // LN sees the value as stored (rounded) so fwd/bwd agree exactly.
+      load8<T>(s_out + base + c, v[i]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sum += v[i][j];
+  }
+  const float mean = wave_sum(sum) / h;
+  float var = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float d = v[i][j] - mean;
+      var += d * d;
+    }
+  const float rstd = rsqrtf(wave_sum(var) / h + eps);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = (i * 64 + lane) * 8;
+    float g[8], b[8], o[8];
+    load8<T>(gamma + c, g);
+    load8<T>(beta + c, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * g[j] + b[j];
+    store8<T>(y + base + c, o);
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// Generic-width fallback (h % 8 == 0): re-reads the row from cache.
+template <typename T>
+__global__ __launch_bounds__(256) void add_ln_fwd_generic(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ bias,
+    const uint16_t* __restrict__ residual, const uint16_t* __restrict__ gamma,
+    const uint16_t* __restrict__ beta, uint16_t* __restrict__ s_out,
+    uint16_t* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+    int rows, int h, float eps, DropCfg drop) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const size_t base = (size_t)row * h;
+  const int nv = h / 8;
+  auto value = [&](int c, float* v) {
+    load8<T>(x + base + c, v);
+    if (bias) {
+      float b[8];
+      load8<T>(bias + c, b);
+      for (int j = 0; j < 8; ++j) v[j] += b[j];
+    }
+    if (drop.enabled)
+      for (int j = 0; j < 8; ++j) v[j] = drop_apply(v[j], base + c + j, drop);
+    if (residual) {
+      float r[8];
+      load8<T>(residual + base + c, r);
+      for (int j = 0; j < 8; ++j) v[j] += r[j];
+    }
+  };
+  float sum = 0.f;
+  for (int vi = lane; vi < nv; vi += 64) {
+    float v[8];
+    value(vi * 8, v);
+    if (s_out) {
+      store8<T>(s_out + base + vi * 8, v);
+      load8<T>(s_out + base + vi * 8, v);
+    }
+    for (int j = 0; j < 8; ++j) sum += v[j];
+  }
+  const float mean = wave_sum(sum) / h;
+  float var = 0.f;
+  for (int vi = lane; vi < nv; vi += 64) {
+    float v[8];
+    if (s_out) load8<T>(s_out + base + vi * 8, v); else value(vi * 8, v);
+    for (int j = 0; j < 8; ++j) { float d = v[j] - mean; var += d * d; }
+  }
+  const float rstd = rsqrtf(wave_sum(var) / h + eps);
+  for (int vi = lane; vi < nv; vi += 64) {
+    float v[8], g[8], b[8], o[8];
+    if (s_out) load8<T>(s_out + base + vi * 8, v); else value(vi * 8, v);
+    load8<T>(gamma + vi * 8, g);
+    load8<T>(beta + vi * 8, b);
+    for (int j = 0; j < 8; ++j) o[j] = (v[j] - mean) * rstd * g[j] + b[j];
+    store8<T>(y + base + vi * 8, o);
+  }
+  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+}
+
+// ---------------------------------------------------------------------------
+// Row backward:  ds = ds_in + LN'(dy);  dx = dropout'(ds)
+//   s: the LN input (as stored), dx_out may alias ds_out when no dropout.
+// ---------------------------------------------------------------------------
+template <typename T, int VPT>
+__global__ __launch_bounds__(256) void ln_bwd_row_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ s,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    const uint16_t* __restrict__ gamma, const uint16_t* __restrict__ ds_in,
+    uint16_t* __restrict__ ds_out, uint16_t* __restrict__ dx_out, int rows, int h,
+    DropCfg drop) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const size_t base = (size_t)row * h;
+  const float mean = mean_in[row], rstd = rstd_in[row];
+  float xh[VPT][8], gdy[VPT][8];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = (i * 64 + lane) * 8;
+    float a[8], g[8], d[8];
+    load8<T>(s + base + c, a);
+    load8<T>(gamma + c, g);
+    load8<T>(dy + base + c, d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      xh[i][j] = (a[j] - mean) * rstd;
+      gdy[i][j] = d[j] * g[j];
+      s1 += gdy[i][j];
+      s2 += gdy[i][j] * xh[i][j];
+    }
+  }
+  const float m1 = wave_sum(s1) / h, m2 = wave_sum(s2) / h;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = (i * 64 + lane) * 8;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = rstd * (gdy[i][j] - m1 - xh[i][j] * m2);
+    if (ds_in) {
+      float r[8];
+      load8<T>(ds_in + base + c, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += r[j];
+    }
+    store8<T>(ds_out + base + c, o);
+    if (drop.enabled) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = drop_apply(o[j], base + c + j, drop);
+      store8<T>(dx_out + base + c, o);
+    } else if (dx_out != ds_out) {
+      store8<T>(dx_out + base + c, o);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ln_bwd_row_generic(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ s,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    const uint16_t* __restrict__ gamma, const uint16_t* __restrict__ ds_in,
+    uint16_t* __restrict__ ds_out, uint16_t* __restrict__ dx_out, int rows, int h,
+    DropCfg drop) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const size_t base = (size_t)row * h;
+  const float mean = mean_in[row], rstd = rstd_in[row];
+  const int nv = h / 8;
+  float s1 = 0.f, s2 = 0.f;
+  for (int vi = lane; vi < nv; vi += 64) {
+    float a[8], g[8], d[8];
+    load8<T>(s + base + vi * 8, a);
+    load8<T>(gamma + vi * 8, g);
+    load8<T>(dy + base + vi * 8, d);
+    for (int j = 0; j < 8; ++j) {
+      float xh = (a[j] - mean) * rstd, gd = d[j] * g[j];
+      s1 += gd;
+      s2 += gd * xh;
+    }
+  }
+  const float m1 = wave_sum(s1) / h, m2 = wave_sum(s2) / h;
+  for (int vi = lane; vi < nv; vi += 64) {
+    const int c = vi * 8;
+    float a[8], g[8], d[8], o[8];
+    load8<T>(s + base + c, a);
+    load8<T>(gamma + c, g);
+    load8<T>(dy + base + c, d);
+    for (int j = 0; j < 8; ++j) o[j] = rstd * (d[j] * g[j] - m1 - (a[j] - mean) * rstd * m2);
+    if (ds_in) {
+      float r[8];
+      load8<T>(ds_in + base + c, r);
+      for (int j = 0; j < 8; ++j) o[j] += r[j];
+    }
+    store8<T>(ds_out + base + c, o);
+    if (drop.enabled) {
+      for (int j = 0; j < 8; ++j) o[j] = drop_apply(o[j], base + c + j, drop);
+      store8<T>(dx_out + base + c, o);
+    } else if (dx_out != ds_out) {
+      store8<T>(dx_out + base + c, o);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Column-tile partial sums.  Block = 256 threads = 16 column groups (8 cols
+// each -> 128 columns) x 16 row lanes.  Grid = (col tiles, splits).
+// MODE 0: LN  -> p0 += dy*xhat, p1 += dy            (a = dy, b = s)
+// MODE 1: sum -> p0 += a                             (plain column sum)
+// ---------------------------------------------------------------------------
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void coltile_partial_kernel(
+    const uint16_t* __restrict__ a, const uint16_t* __restrict__ b,
+    const float* __restrict__ mean, const float* __restrict__ rstd,
+    float* __restrict__ p0, float* __restrict__ p1, int rows, int cols, int rows_per_split) {
+  __shared__ float red[2][16][129];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int col = blockIdx.x * 128 + tx * 8;
+  const int r0 = blockIdx.y * rows_per_split;
+  const int r1 = min(rows, r0 + rows_per_split);
+  float acc0[8], acc1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc0[j] = acc1[j] = 0.f;
+  if (col < cols) {
+    for (int r = r0 + ty; r < r1; r += 16) {
+      const size_t off = (size_t)r * cols + col;
+      float va[8];
+      load8<T>(a + off, va);
+      if (MODE == 0) {
+        float vb[8];
+        load8<T>(b + off, vb);
+        const float m = mean[r], rs = rstd[r];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          acc0[j] += va[j] * (vb[j] - m) * rs;
+          acc1[j] += va[j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc0[j] += va[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][ty][tx * 8 + j] = acc0[j];
+    red[1][ty][tx * 8 + j] = acc1[j];
+  }
+  __syncthreads();
+  // 256 threads reduce 128 columns x 2 arrays over 16 rows
+  const int which = threadIdx.x >> 7, c = threadIdx.x & 127;
+  if (MODE == 1 && which == 1) return;
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) s += red[which][t][c];
+  const int gc = blockIdx.x * 128 + c;
+  if (gc < cols) (which == 0 ? p0 : p1)[(size_t)blockIdx.y * cols + gc] = s;
+}
+
+// Sum partials over splits; write fp32 and/or 16-bit outputs.
+template <typename T>
+__global__ void coltile_finalize_kernel(const float* __restrict__ p, int splits, int cols,
+                                        float* __restrict__ out_f32, uint16_t* __restrict__ out_t,
+                                        int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += p[(size_t)k * cols + c];
+  if (out_f32) out_f32[c] = accumulate ? out_f32[c] + s : s;
+  if (out_t) out_t[c] = Elt<T>::from_f(s);
+}
+
+// ---------------------------------------------------------------------------
+// bias + GeLU  (fwd stores y; bwd emits dx and column partials of dx)
+// ---------------------------------------------------------------------------
+template <typename T, bool ERF>
+__global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ bias, uint16_t* __restrict__ y,
+    long n8, int cols) {
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < n8; v += (long)gridDim.x * blockDim.x) {
+    const long off = v * 8;
+    const int c = (int)(off % cols);
+    float a[8], b[8];
+    load8<T>(x + off, a);
+    if (bias) load8<T>(bias + c, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = a[j] + (bias ? b[j] : 0.f);
+      a[j] = ERF ? gelu_erf(t) : gelu_tanh(t);
+    }
+    store8<T>(y + off, a);
+  }
+}
+
+template <typename T, bool ERF>
+__global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+    const uint16_t* __restrict__ bias, uint16_t* __restrict__ dx, float* __restrict__ part,
+    int rows, int cols, int rows_per_split) {
+  __shared__ float red[16][129];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int col = blockIdx.x * 128 + tx * 8;
+  const int r0 = blockIdx.y * rows_per_split;
+  const int r1 = min(rows, r0 + rows_per_split);
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  if (col < cols) {
+    float b[8];
+    if (bias) load8<T>(bias + col, b);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b[j] = 0.f;
+    }
+    for (int r = r0 + ty; r < r1; r += 16) {
+      const size_t off = (size_t)r * cols + col;
+      float g[8], a[8];
+      load8<T>(dy + off, g);
+      load8<T>(x + off, a);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = a[j] + b[j];
+        g[j] *= ERF ? gelu_erf_grad(t) : gelu_tanh_grad(t);
+      }
+      store8<T>(dx + off, g);
+      // accumulate the rounded value so dbias == colsum(dx) exactly
+      load8<T>(dx + off, g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += g[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[ty][tx * 8 + j] = acc[j];
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) s += red[t][threadIdx.x];
+    const int gc = blockIdx.x * 128 + threadIdx.x;
+    if (part && gc < cols) part[(size_t)blockIdx.y * cols + gc] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// out = residual + dropout(x + bias)      and its backward
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void bias_dropout_add_fwd_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ bias,
+    const uint16_t* __restrict__ residual, uint16_t* __restrict__ out, long n8, int cols,
+    DropCfg drop) {
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < n8; v += (long)gridDim.x * blockDim.x) {
+    const long off = v * 8;
+    const int c = (int)(off % cols);
+    float a[8];
+    load8<T>(x + off, a);
+    if (bias) {
+      float b[8];
+      load8<T>(bias + c, b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += b[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = drop_apply(a[j], (uint64_t)off + j, drop);
+    if (residual) {
+      float r[8];
+      load8<T>(residual + off, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += r[j];
+    }
+    store8<T>(out + off, a);
+  }
+}
+
+// dx = dropout'(dout); column partials of dx (for dbias) if part != null.
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_bwd_colsum_kernel(
+    const uint16_t* __restrict__ dout, uint16_t* __restrict__ dx, float* __restrict__ part,
+    int rows, int cols, int rows_per_split, DropCfg drop) {
+  __shared__ float red[16][129];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int col = blockIdx.x * 128 + tx * 8;
+  const int r0 = blockIdx.y * rows_per_split;
+  const int r1 = min(rows, r0 + rows_per_split);
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  if (col < cols) {
+    for (int r = r0 + ty; r < r1; r += 16) {
+      const size_t off = (size_t)r * cols + col;
+      float g[8];
+      load8<T>(dout + off, g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = drop_apply(g[j], off + j, drop);
+      if (dx) {
+        store8<T>(dx + off, g);
+        load8<T>(dx + off, g);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += g[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[ty][tx * 8 + j] = acc[j];
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) s += red[t][threadIdx.x];
+    const int gc = blockIdx.x * 128 + threadIdx.x;
+    if (part && gc < cols) part[(size_t)blockIdx.y * cols + gc] = s;
+  }
+}
+
+// Plain dropout (embedding / generic): y = dropout(x)
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_fwd_kernel(const uint16_t* __restrict__ x,
+                                                          uint16_t* __restrict__ y, long n8,
+                                                          DropCfg drop) {
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < n8; v += (long)gridDim.x * blockDim.x) {
+    const long off = v * 8;
+    float a[8];
+    load8<T>(x + off, a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = drop_apply(a[j], (uint64_t)off + j, drop);
+    store8<T>(y + off, a);
+  }
+}
+
+DropCfg make_drop(float p, uint64_t key) {
+  DropCfg d;
+  d.enabled = p > 0.f ? 1 : 0;
+  d.klo = (uint32_t)(key & 0xffffffffu);
+  d.khi = (uint32_t)(key >> 32);
+  d.thr = (uint32_t)(p * 65536.0f + 0.5f);
+  d.scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  return d;
+}
+
+inline int grid_for(long n8) {
+  long g = (n8 + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+inline int splits_for(int rows, int cols) {
+  int tiles = (cols + 127) / 128;
+  int s = 1024 / (tiles > 0 ? tiles : 1);
+  if (s < 1) s = 1;
+  int max_s = (rows + 15) / 16;
+  if (s > max_s) s = max_s;
+  if (s > 512) s = 512;
+  return s;
+}
+
+}  // namespace
+
+// ============================================================================
+// host launchers (extern "C" ABI, called from the pybind module)
+// dtype: 0 = bf16, 1 = fp16
+// ============================================================================
+#define FX_DISPATCH_T(dtype, ...)        \
+  if (dtype == 0) {                      \
+    using T = bf16;                      \
+    __VA_ARGS__;                         \
+  } else {                               \
+    using T = f16;                       \
+    __VA_ARGS__;                         \
+  }
+
+extern "C" int fx_coltile_splits(int rows, int cols) { return splits_for(rows, cols); }
+
+extern "C" void fx_add_ln_fwd(int dtype, const void* x, const void* bias, const void* residual,
+                              const void* gamma, const void* beta, void* s_out, void* y,
+                              float* mean, float* rstd, int rows, int h, float eps, float p,
+                              uint64_t key, hipStream_t st) {
+  DropCfg d = make_drop(p, key);
+  dim3 grid((rows + 3) / 4), block(256);
+  auto X = (const uint16_t*)x;
+  auto B = (const uint16_t*)bias;
+  auto R = (const uint16_t*)residual;
+  auto G = (const uint16_t*)gamma;
+  auto Be = (const uint16_t*)beta;
+  auto S = (uint16_t*)s_out;
+  auto Y = (uint16_t*)y;
+#define LN_CASE(V)                                                                          \
+  case V:                                                                                   \
+    FX_DISPATCH_T(dtype, add_ln_fwd_kernel<T, V><<<grid, block, 0, st>>>(                   \
+                             X, B, R, G, Be, S, Y, mean, rstd, rows, h, eps, d));           \
+    break;
+  if (h % 512 == 0 && h / 512 <= 16) {
+    switch (h / 512) {
+      LN_CASE(1) LN_CASE(2) LN_CASE(3) LN_CASE(4) LN_CASE(5) LN_CASE(6) LN_CASE(7) LN_CASE(8)
+      LN_CASE(10) LN_CASE(12) LN_CASE(16)
+      default:
+        FX_DISPATCH_T(dtype, add_ln_fwd_generic<T><<<grid, block, 0, st>>>(
+                                 X, B, R, G, Be, S, Y, mean, rstd, rows, h, eps, d));
+    }
+  } else {
+    FX_DISPATCH_T(dtype, add_ln_fwd_generic<T><<<grid, block, 0, st>>>(
+                             X, B, R, G, Be, S, Y, mean, rstd, rows, h, eps, d));
+  }
+#undef LN_CASE
+}
+
+extern "C" void fx_ln_bwd_row(int dtype, const void* dy, const void* s, const float* mean,
+                              const float* rstd, const void* gamma, const void* ds_in,
+                              void* ds_out, void* dx_out, int rows, int h, float p, uint64_t key,
+                              hipStream_t st) {
+  DropCfg d = make_drop(p, key);
+  dim3 grid((rows + 3) / 4), block(256);
+  auto DY = (const uint16_t*)dy;
+  auto S = (const uint16_t*)s;
+  auto G = (const uint16_t*)gamma;
+  auto DI = (const uint16_t*)ds_in;
+  auto DS = (uint16_t*)ds_out;
+  auto DX = (uint16_t*)dx_out;
+#define LNB_CASE(V)                                                                       \
+  case V:                                                                                 \
+    FX_DISPATCH_T(dtype, ln_bwd_row_kernel<T, V><<<grid, block, 0, st>>>(                 \
+                             DY, S, mean, rstd, G, DI, DS, DX, rows, h, d));              \
+    break;
+  if (h % 512 == 0 && h / 512 <= 8) {
+    switch (h / 512) {
+      LNB_CASE(1) LNB_CASE(2) LNB_CASE(3) LNB_CASE(4) LNB_CASE(5) LNB_CASE(6) LNB_CASE(7)
+      LNB_CASE(8)
+      default:
+        FX_DISPATCH_T(dtype, ln_bwd_row_generic<T><<<grid, block, 0, st>>>(
+                                 DY, S, mean, rstd, G, DI, DS, DX, rows, h, d));
+    }
+  } else {
+    FX_DISPATCH_T(dtype, ln_bwd_row_generic<T><<<grid, block, 0, st>>>(
+                             DY, S, mean, rstd, G, DI, DS, DX, rows, h, d));
+  }
+#undef LNB_CASE
+}
+
+// dgamma/dbeta partials (mode 0) or plain column sum partials (mode 1).
+extern "C" void fx_coltile_partial(int dtype, int mode, const void* a, const void* b,
+                                   const float* mean, const float* rstd, float* p0, float* p1,
+                                   int rows, int cols, int splits, hipStream_t st) {
+  int rps = (rows + splits - 1) / splits;
+  dim3 grid((cols + 127) / 128, splits), block(256);
+  auto A = (const uint16_t*)a;
+  auto B = (const uint16_t*)b;
+  if (mode == 0) {
+    FX_DISPATCH_T(dtype, coltile_partial_kernel<T, 0><<<grid, block, 0, st>>>(
+                             A, B, mean, rstd, p0, p1, rows, cols, rps));
+  } else {
+    FX_DISPATCH_T(dtype, coltile_partial_kernel<T, 1><<<grid, block, 0, st>>>(
+                             A, B, mean, rstd, p0, p1, rows, cols, rps));
+  }
+}
+
+extern "C" void fx_coltile_finalize(int dtype, const float* part, int splits, int cols,
+                                    float* out_f32, void* out_t, int accumulate, hipStream_t st) {
+  dim3 grid((cols + 255) / 256), block(256);
+  FX_DISPATCH_T(dtype, coltile_finalize_kernel<T><<<grid, block, 0, st>>>(
+                           part, splits, cols, out_f32, (uint16_t*)out_t, accumulate));
+}
+
+extern "C" void fx_bias_gelu_fwd(int dtype, int erf, const void* x, const void* bias, void* y,
+                                 long n, int cols, hipStream_t st) {
+  long n8 = n / 8;
+  if (erf) {
+    FX_DISPATCH_T(dtype, bias_gelu_fwd_kernel<T, true><<<grid_for(n8), 256, 0, st>>>(
+                             (const uint16_t*)x, (const uint16_t*)bias, (uint16_t*)y, n8, cols));
+  } else {
+    FX_DISPATCH_T(dtype, bias_gelu_fwd_kernel<T, false><<<grid_for(n8), 256, 0, st>>>(
+                             (const uint16_t*)x, (const uint16_t*)bias, (uint16_t*)y, n8, cols));
+  }
+}
+
+extern "C" void fx_bias_gelu_bwd(int dtype, int erf, const void* dy, const void* x,
+                                 const void* bias, void* dx, float* part, int rows, int cols,
+                                 int splits, hipStream_t st) {
+  int rps = (rows + splits - 1) / splits;
+  dim3 grid((cols + 127) / 128, splits), block(256);
+  if (erf) {
+    FX_DISPATCH_T(dtype, bias_gelu_bwd_kernel<T, true><<<grid, block, 0, st>>>(
+                             (const uint16_t*)dy, (const uint16_t*)x, (const uint16_t*)bias,
+                             (uint16_t*)dx, part, rows, cols, rps));
+  } else {
+    FX_DISPATCH_T(dtype, bias_gelu_bwd_kernel<T, false><<<grid, block, 0, st>>>(
+                             (const uint16_t*)dy, (const uint16_t*)x, (const uint16_t*)bias,
+                             (uint16_t*)dx, part, rows, cols, rps));
+  }
+}
+
+extern "C" void fx_bias_dropout_add_fwd(int dtype, const void* x, const void* bias,
+                                        const void* residual, void* out, long n, int cols, float p,
+                                        uint64_t key, hipStream_t st) {
+  DropCfg d = make_drop(p, key);
+  long n8 = n / 8;
+  FX_DISPATCH_T(dtype, bias_dropout_add_fwd_kernel<T><<<grid_for(n8), 256, 0, st>>>(
+                           (const uint16_t*)x, (const uint16_t*)bias, (const uint16_t*)residual,
+                           (uint16_t*)out, n8, cols, d));
+}
+
+extern "C" void fx_dropout_bwd_colsum(int dtype, const void* dout, void* dx, float* part,
+                                      int rows, int cols, int splits, float p, uint64_t key,
+                                      hipStream_t st) {
+  DropCfg d = make_drop(p, key);
+  int rps = (rows + splits - 1) / splits;
+  dim3 grid((cols + 127) / 128, splits), block(256);
+  FX_DISPATCH_T(dtype, dropout_bwd_colsum_kernel<T><<<grid, block, 0, st>>>(
+                           (const uint16_t*)dout, (uint16_t*)dx, part, rows, cols, rps, d));
+}
+
+extern "C" void fx_dropout_fwd(int dtype, const void* x, void* y, long n, float p, uint64_t key,
+                               hipStream_t st) {
+  DropCfg d = make_drop(p, key);
+  long n8 = n / 8;
+  FX_DISPATCH_T(dtype, dropout_fwd_kernel<T><<<grid_for(n8), 256, 0, st>>>(
+                           (const uint16_t*)x, (uint16_t*)y, n8, d));
+}

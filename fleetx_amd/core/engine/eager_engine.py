@@ -1,0 +1,420 @@
+"""EagerEngine: the train / eval / predict / save / load / export loop.
+
+Parity: reference ``core/engine/eager_engine.py:41-738`` (C15).  Config keys
+read: ``Engine.{run_mode, max_steps, num_train_epochs, eval_freq, eval_iters,
+test_iters, logging_freq, accumulate_steps, mix_precision.*, save_load.*}``,
+``Distributed.*``, ``Profiler.*``, ``Inference.*``.
+
+MI355X-first differences:
+* model parameters live in one flat bf16 buffer with fp32 ``main_grad``
+  views (:mod:`fleetx_amd.parallel.grad_buffer`); DP / ZeRO gradient
+  collectives are bucketed and launched from backward hooks, so they overlap
+  with the rest of backward instead of the reference's post-backward
+  ``fused_allreduce_gradients``;
+* gradient accumulation (``local_batch_size / micro_batch_size``) works for
+  every layout (the reference only accumulated under pipeline parallelism,
+  SURVEY §2.12 #3);
+* the host only synchronises at ``logging_freq`` (the reference synced and
+  copied the loss every step, §2.12 #12);
+* bf16 by default (no loss scaling); the fp16 path keeps a device-side
+  dynamic loss scaler (init 32768, x2 every 1000 good steps, /2 on overflow);
+* resume seeks the batch sampler via ``consumed_samples`` instead of reading
+  and discarding batches (§2.12 #10), and restores the dropout RNG streams.
+"""
+import contextlib
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .basic_engine import BasicEngine
+from ...optims import build_optimizer, build_lr_scheduler
+from ...parallel import topology as topo
+from ...parallel.grad_buffer import FlatParamGradBuffer
+from ...parallel.rng import get_rng_state_tracker
+from ...utils import checkpoint as ckpt
+from ...utils import env
+from ...utils.log import logger
+
+
+class DynamicLossScaler:
+    """Device-resident GradScaler (reference K14; ``eager_engine.py:157-167``)."""
+
+    def __init__(self, init_scale=32768.0, incr_every=1000, incr_ratio=2.0, decr_ratio=0.5,
+                 device="cpu"):
+        self.scale = torch.full((), float(init_scale), dtype=torch.float32, device=device)
+        self.good = torch.zeros((), dtype=torch.int32, device=device)
+        self.incr_every, self.incr_ratio, self.decr_ratio = incr_every, incr_ratio, decr_ratio
+
+    def update(self, found_inf):
+        inf = found_inf.reshape(()).bool()
+        self.good = torch.where(inf, torch.zeros_like(self.good), self.good + 1)
+        grow = self.good >= self.incr_every
+        self.scale = torch.where(inf, self.scale * self.decr_ratio,
+                                 torch.where(grow, self.scale * self.incr_ratio, self.scale))
+        self.good = torch.where(grow, torch.zeros_like(self.good), self.good)
+
+    def state_dict(self):
+        return {"scale": self.scale.cpu(), "good": self.good.cpu()}
+
+    def load_state_dict(self, s):
+        self.scale.copy_(s["scale"])
+        self.good.copy_(s["good"])
+
+
+def _to_device(batch, device):
+    if torch.is_tensor(batch):
+        return batch.to(device, non_blocking=True)
+    if isinstance(batch, (list, tuple)):
+        return type(batch)(_to_device(b, device) for b in batch)
+    if isinstance(batch, dict):
+        return {k: _to_device(v, device) for k, v in batch.items()}
+    return batch
+
+
+def _split_micro(batch, n):
+    if n == 1:
+        return [batch]
+    if torch.is_tensor(batch):
+        assert batch.shape[0] % n == 0, "batch {} not divisible into {} micro-batches".format(
+            batch.shape[0], n)
+        return list(batch.chunk(n, dim=0))
+    if isinstance(batch, (list, tuple)):
+        parts = [_split_micro(b, n) for b in batch]
+        return [type(batch)(p[i] for p in parts) for i in range(n)]
+    return [batch] * n
+
+
+class EagerEngine(BasicEngine):
+    def __init__(self, configs, module, optimizer=None, lr=None, mode="train"):
+        super().__init__()
+        self.mode = mode
+        self._configs = configs
+        self._module = module
+        e = configs.Engine
+        self._run_mode = e.get("run_mode", "step")
+        assert self._run_mode in ("epoch", "step"), "run_mode must be epoch or step"
+        self._max_steps = e.get("max_steps", 1)
+        self._eval_freq = e.get("eval_freq", 1) or 1
+        self._eval_iters = e.get("eval_iters", 10)
+        self._test_iters = e.get("test_iters", 100)
+        self._logging_freq = e.get("logging_freq", 1) or 1
+        self._num_train_epochs = e.get("num_train_epochs", 1)
+        self._accumulate_steps = e.get("accumulate_steps", 1) or 1
+        amp = e.get("mix_precision", {}) or {}
+        self._use_pure_fp16 = bool(amp.get("use_pure_fp16", False))
+        sl = e.get("save_load", {}) or {}
+        self._save_steps = sl.get("save_steps", sys.maxsize)
+        self._save_epoch = sl.get("save_epoch", 1)
+        self._output_dir = sl.get("output_dir", "./output")
+        self._ckpt_dir = sl.get("ckpt_dir")
+        self._nan_guard = e.get("nan_guard", "off")
+        self._fault = os.environ.get("FLEETX_FAULT_INJECT")  # "rank:step" -> os._exit(17)
+
+        self.hcg = topo.get_hcg()
+        self._dp_rank = self.hcg.dp_rank
+        self._mp_rank, self._pp_rank = self.hcg.mp_rank, self.hcg.pp_rank
+        self._sharding_rank = self.hcg.sharding_rank
+        self._distributed = self.hcg.topo.world_size > 1
+        sh = configs.Distributed.sharding
+        self._sharding_stage = sh.get("sharding_stage", 1) if sh.get("sharding_degree", 1) > 1 else 0
+        self.device = env.device()
+
+        model = module.model
+        from ...models.language_model.language_module import compute_dtype
+        self._dtype = compute_dtype(configs)
+        model.to(self.device)
+        if mode == "export":
+            self._dtype = torch.float32  # reference: pure fp16 disabled for export
+        model.to(self._dtype)
+        self._pipeline = hasattr(model, "train_batch")
+
+        self.buffer, self.optimizer, self.lr_scheduler = None, optimizer, lr
+        self.scaler = None
+        if mode == "train":
+            comm = configs.Distributed.get("comm", {}) or {}
+            sh_grp = self.hcg.get_sharding_parallel_group() if self._sharding_stage >= 1 else None
+            self.buffer = FlatParamGradBuffer(
+                model.named_parameters(), dp_group=self.hcg.get_data_parallel_group(),
+                shard_group=sh_grp if sh_grp is not None else self.hcg.get_sharding_parallel_group(),
+                mp_group=self.hcg.get_model_parallel_group(),
+                embed_group=self.hcg.get_embedding_group() if self.hcg.pp_degree > 1 else None,
+                bucket_mb=comm.get("dp_bucket_mb", 256),
+                overlap=comm.get("overlap_grad_reduce", True),
+                shard_stage=self._sharding_stage)
+            if self.lr_scheduler is None and "lr" in configs.Optimizer:
+                self.lr_scheduler = build_lr_scheduler(configs.Optimizer.lr)
+            self.optimizer = build_optimizer(configs.Optimizer, self.buffer, self.lr_scheduler,
+                                             mp_group=self.hcg.get_model_parallel_group(),
+                                             pp_group=self.hcg.get_pipe_parallel_group())
+            if self._use_pure_fp16 and self._dtype == torch.float16:
+                self.scaler = DynamicLossScaler(amp.get("scale_loss", 32768.0), device=self.device)
+                self.optimizer.loss_scale = self.scaler.scale
+            if self._pipeline:
+                model.attach(self)
+        self._profiler = self._build_profiler(configs.get("Profiler"))
+        self._inference_engine = None
+        self.consumed_samples = 0
+        if mode == "inference":
+            inf = configs.get("Inference", {}) or {}
+            self._inference_model_dir = inf.get("model_dir", self._output_dir)
+
+    # ------------------------------------------------------------------ profiler
+    def _build_profiler(self, pcfg):
+        if not pcfg or not pcfg.get("enable", False):
+            return None
+        from ...utils.profiler import Profiler
+        return Profiler(pcfg)
+
+    # ------------------------------------------------------------------ train
+    def _fault_check(self, step):
+        if self._fault:
+            r, s = self._fault.split(":")
+            if int(r) == env.get_rank() and int(s) == step:
+                logger.error("fault injection: rank %s exits at step %s" % (r, s))
+                os._exit(17)
+
+    def _fit_impl(self, batch):
+        model = self._module.model
+        model.train()
+        if self._pipeline:
+            loss = model.train_batch(self._module.pretreating_batch(batch), self._accumulate_steps)
+        else:
+            micro = _split_micro(batch, self._accumulate_steps)
+            loss = None
+            for i, mb in enumerate(micro):
+                self.buffer.set_last_micro_batch(i == len(micro) - 1)
+                l = self._module.training_step(mb)
+                if self._accumulate_steps > 1:
+                    l = l / self._accumulate_steps
+                self._module.backward(l * self.scaler.scale if self.scaler is not None else l)
+                loss = l.detach() if loss is None else loss + l.detach()
+        self.buffer.finish()
+        self._optim_update()
+        return loss
+
+    def _optim_update(self):
+        self.optimizer.step()
+        if self.scaler is not None:
+            self.scaler.update(self.optimizer.found_inf)
+            self.optimizer.loss_scale = self.scaler.scale
+        if self.lr_scheduler is not None and hasattr(self.lr_scheduler, "step"):
+            self.lr_scheduler.step()
+        self.optimizer.clear_grad()
+
+    def _current_lr(self):
+        return self.optimizer.get_lr() if self.optimizer is not None else 0.0
+
+    def fit(self, epoch=1, train_data_loader=None, valid_data_loader=None):
+        assert self.mode == "train"
+        start_epoch = getattr(self, "_load_recovery", {}).get("epoch", 0)
+        start_step = getattr(self, "_load_recovery", {}).get("step", 0)
+        if self._profiler:
+            self._profiler.start()
+        global_step = start_step
+        for ep in range(start_epoch, epoch if self._run_mode == "epoch" else max(epoch, 1)):
+            sampler = getattr(train_data_loader, "batch_sampler", None)
+            if sampler is not None and hasattr(sampler, "set_epoch"):
+                sampler.set_epoch(ep, self.consumed_samples if ep == start_epoch else 0)
+            t_epoch = time.time()
+            global_step, done = self._train_one_epoch(ep, train_data_loader, valid_data_loader,
+                                                      global_step)
+            self._module.training_epoch_end({"epoch": ep, "train_cost": time.time() - t_epoch})
+            if self._run_mode == "epoch" and (ep + 1) % self._save_epoch == 0:
+                self.save(epoch=ep + 1, step=global_step)
+            if done:
+                break
+        if self._profiler:
+            self._profiler.stop()
+        return global_step
+
+    def _train_one_epoch(self, epoch, loader, valid_loader, global_step):
+        gbs = self._configs.Global.global_batch_size
+        loss_acc, n_acc = None, 0
+        t0 = time.time()
+        for batch in loader:
+            self._fault_check(global_step)
+            batch = _to_device(batch, self.device)
+            loss = self._fit_impl(batch)
+            global_step += 1
+            self.consumed_samples += gbs
+            if loss is not None:
+                loss_acc = loss if loss_acc is None else loss_acc + loss
+                n_acc += 1
+            if global_step % self._logging_freq == 0:
+                if torch.cuda.is_available():
+                    torch.cuda.synchronize()
+                cost = (time.time() - t0) / self._logging_freq
+                lval = self._reduce_log_loss(loss_acc, n_acc)
+                if self._nan_guard != "off" and not np.isfinite(lval):
+                    msg = "non-finite loss at step %d" % global_step
+                    if self._nan_guard == "abort":
+                        raise FloatingPointError(msg)
+                    logger.warning(msg)
+                self._module.training_step_end({"epoch": epoch, "batch": global_step, "loss": lval,
+                                                "train_cost": cost, "lr": self._current_lr()})
+                loss_acc, n_acc = None, 0
+                t0 = time.time()
+            if self._run_mode == "step" and valid_loader is not None and \
+                    global_step % self._eval_freq == 0:
+                self._evaluate_impl(epoch, valid_loader, self._eval_iters)
+                t0 = time.time()
+            if self._run_mode == "step" and global_step % self._save_steps == 0:
+                self.save(epoch=epoch, step=global_step)
+            if self._profiler:
+                self._profiler.step()
+            if self._run_mode == "step" and global_step >= self._max_steps:
+                return global_step, True
+        return global_step, False
+
+    def _reduce_log_loss(self, loss_acc, n):
+        """Loss for the log line: mean over the window; under PP it lives on
+        the last stage and is broadcast to all stages."""
+        if loss_acc is None:
+            v = torch.zeros((), device=self.device)
+        else:
+            v = (loss_acc / max(n, 1)).float()
+        if self.hcg.pp_degree > 1:
+            g = self.hcg.get_pipe_parallel_group()
+            src = g.ranks[-1]
+            v = v.clone()
+            dist.broadcast(v, src=src, group=g.group)
+        return float(v.item())
+
+    # ------------------------------------------------------------------ eval
+    @torch.no_grad()
+    def _evaluate_impl(self, epoch, loader, iters):
+        model = self._module.model
+        model.eval()
+        outs = []
+        t0 = time.time()
+        for i, batch in enumerate(loader):
+            if i >= iters:
+                break
+            batch = _to_device(batch, self.device)
+            if self._pipeline:
+                loss = model.eval_batch(self._module.pretreating_batch(batch))
+            else:
+                loss = self._module.validation_step(batch)
+            outs.append(loss)
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            cost = time.time() - t0
+            if (i + 1) % self._logging_freq == 0:
+                lval = float(loss.float().item()) if torch.is_tensor(loss) else loss
+                self._module.validation_step_end({"epoch": epoch, "batch": i, "loss": lval,
+                                                  "eval_cost": cost / self._logging_freq})
+                t0 = time.time()
+        model.train()
+        return outs
+
+    def evaluate(self, epoch=1, valid_data_loader=None):
+        model = self._module.model
+        model.eval()
+        outs = []
+        t0 = time.time()
+        with torch.no_grad():
+            for i, batch in enumerate(valid_data_loader):
+                batch = _to_device(batch, self.device)
+                out = self._module.validation_step(batch)
+                self._module.validation_step_end({"epoch": epoch, "batch": i, "loss": out,
+                                                  "eval_cost": time.time() - t0})
+                outs.append(out)
+                t0 = time.time()
+        self._module.validation_epoch_end({"epoch": epoch})
+        return outs
+
+    @torch.no_grad()
+    def predict(self, epoch=1, test_data_loader=None):
+        model = self._module.model
+        model.eval()
+        outs = []
+        t0 = time.time()
+        for i, batch in enumerate(test_data_loader):
+            if i >= self._test_iters:
+                break
+            batch = _to_device(batch, self.device)
+            out = self._module.test_step(batch)
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            lval = float(out.float().item()) if torch.is_tensor(out) and out.numel() == 1 else 0.0
+            self._module.test_step_end({"epoch": epoch, "batch": i, "loss": lval,
+                                        "test_cost": time.time() - t0})
+            outs.append(out)
+            t0 = time.time()
+        return outs
+
+    # ------------------------------------------------------------------ save/load
+    def _shard_dir(self, base):
+        if self._distributed:
+            return os.path.join(base, ckpt.shard_dirname(self._mp_rank, self._sharding_rank,
+                                                         self._pp_rank))
+        return base
+
+    def save(self, epoch=0, step=0):
+        if self._dp_rank != 0:
+            return
+        target = self._shard_dir(ckpt.step_dir(self._output_dir, epoch, step))
+        model_sd = {k: v.detach().cpu() for k, v in self._module.model.state_dict().items()}
+        payloads = {"model.pdparams": model_sd}
+        if self.optimizer is not None:
+            payloads["model_state.pdopt"] = self.optimizer.state_dict()
+        meta = {"epoch": epoch, "step": step, "consumed_samples": self.consumed_samples,
+                "rng_tracker": get_rng_state_tracker().get_states()}
+        if self.scaler is not None:
+            meta["scaler"] = self.scaler.state_dict()
+        if torch.cuda.is_available():
+            meta["cuda_rng_state"] = torch.cuda.get_rng_state()
+        payloads["meta_state.pdopt"] = meta
+        ckpt.save_payloads(target, payloads)
+        logger.info("Save model to %s" % target)
+
+    def load(self, ckpt_dir=None):
+        ckpt_dir = ckpt_dir or self._ckpt_dir
+        if not ckpt_dir:
+            return
+        if ckpt_dir == "auto":
+            ckpt_dir = ckpt.latest_checkpoint(self._output_dir)
+            if ckpt_dir is None:
+                logger.info("no checkpoint to resume from in %s" % self._output_dir)
+                return
+        d = self._shard_dir(ckpt_dir)
+        if not os.path.isdir(d):
+            d = ckpt_dir
+        mp = os.path.join(d, "model.pdparams")
+        if not os.path.isfile(mp):
+            raise FileNotFoundError("{} not found".format(mp))
+        sd = ckpt.load_payload(mp)
+        self._module.model.load_state_dict(sd, strict=False)
+        if self.mode == "train":
+            op, mt = os.path.join(d, "model_state.pdopt"), os.path.join(d, "meta_state.pdopt")
+            if not (os.path.isfile(op) and os.path.isfile(mt)):
+                raise FileNotFoundError("optimizer/meta state missing in {}".format(d))
+            self.optimizer.set_state_dict(ckpt.load_payload(op))
+            meta = ckpt.load_payload(mt)
+            self._load_recovery = {"epoch": meta.get("epoch", 0), "step": meta.get("step", 0)}
+            self.consumed_samples = int(meta.get("consumed_samples", 0))
+            if "rng_tracker" in meta:
+                get_rng_state_tracker().set_states(meta["rng_tracker"])
+            if self.scaler is not None and "scaler" in meta:
+                self.scaler.load_state_dict(meta["scaler"])
+            if "cuda_rng_state" in meta and torch.cuda.is_available():
+                torch.cuda.set_rng_state(meta["cuda_rng_state"])
+        logger.info("Load checkpoint from %s" % d)
+
+    # ------------------------------------------------------------------ export / inference
+    def export(self):
+        from ...utils.export import export_inference_model
+        out = os.path.join(self._output_dir, "rank_{}".format(self._dp_rank))
+        export_inference_model(self._module, out)
+        logger.info("export model to %s" % out)
+
+    def inference(self, data):
+        if self._inference_engine is None:
+            from .inference_engine import InferenceEngine
+            self._inference_engine = InferenceEngine(self._inference_model_dir,
+                                                     self.hcg.mp_degree)
+        return self._inference_engine.predict(data)

@@ -1,0 +1,15 @@
+"""Dataset registry."""
+from .gpt_dataset import (GPTDataset, SyntheticGPTDataset, LM_Eval_Dataset,  # noqa: F401
+                          Lambada_Eval_Dataset)
+
+DATASETS = {
+    "GPTDataset": GPTDataset,
+    "SyntheticGPTDataset": SyntheticGPTDataset,
+    "LM_Eval_Dataset": LM_Eval_Dataset,
+    "Lambada_Eval_Dataset": Lambada_Eval_Dataset,
+}
+
+
+def register_dataset(name, cls):
+    DATASETS[name] = cls
+    return cls

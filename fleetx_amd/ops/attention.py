@@ -1,0 +1,160 @@
+"""Fused multi-head attention (flash-style) on the HIP kernels.
+
+Reference K03-K06 (``single_model.py:189-213``, ``hybrid_model.py:268-298``):
+scaled QK^T, causal softmax (``softmax_mask_fuse_upper_triangle``),
+attention-prob dropout under the ``local_seed`` stream, PV and head merge.
+
+Layouts are passed as strides, so the packed QKV GEMM output
+``[b, s, heads, 3, d]`` (per-head interleave, which is what a column-split
+QKV weight produces under tensor parallelism) is consumed without a
+transpose/split copy, and the backward writes ``dq/dk/dv`` straight into one
+packed gradient buffer.  The sequence-parallel ``[s, b, ...]`` layout works
+the same way (only strides differ).
+"""
+import math
+
+import torch
+
+from . import _lib
+from ..parallel import rng as _rng
+
+
+def _strides(t):
+    # t: [B, S, H, D] view
+    return [t.stride(0), t.stride(1), t.stride(2)]
+
+
+def attention_reference(q, k, v, causal=True, dropout_p=0.0, key=0, scale=None, kv_lens=None):
+    """PyTorch math for ``[B, S, H, D]`` inputs (CPU path and test oracle)."""
+    B, Sq, H, D = q.shape
+    Sk = k.shape[1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    qf = q.float().permute(0, 2, 1, 3)
+    kf = k.float().permute(0, 2, 1, 3)
+    vf = v.float().permute(0, 2, 1, 3)
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    mask = torch.zeros(Sq, Sk, dtype=torch.bool, device=q.device)
+    if causal:
+        mask = torch.triu(torch.ones(Sq, Sk, dtype=torch.bool, device=q.device), diagonal=1)
+    mask = mask.view(1, 1, Sq, Sk).expand(B, H, Sq, Sk)
+    if kv_lens is not None:
+        kl = kv_lens.to(q.device).view(B, 1, 1, 1)
+        mask = mask | (torch.arange(Sk, device=q.device).view(1, 1, 1, Sk) >= kl)
+    s = s.masked_fill(mask, float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    p = torch.nan_to_num(p, nan=0.0)
+    if dropout_p > 0.0:
+        keep = _rng.attention_keep_mask(B * H, Sq, Sk, dropout_p, key, q.device).view(B, H, Sq, Sk)
+        p = torch.where(keep, p / (1.0 - dropout_p), torch.zeros_like(p))
+    o = torch.matmul(p, vf).permute(0, 2, 1, 3)
+    return o.to(q.dtype)
+
+
+class _FlashAttn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, packed, causal, p, key, scale, kv_lens):
+        # packed: None or the [B,S,H,3,D] tensor q/k/v are views of
+        B, Sq, H, D = q.shape
+        Sk = k.shape[1]
+        if D not in (64, 128):
+            raise NotImplementedError("flash attention supports head_dim 64/128 (got %d)" % D)
+        for t in (q, k, v):
+            if t.stride(-1) != 1:
+                raise ValueError("head dim must be contiguous")
+        k_ = _lib.kernels()
+        out = torch.empty(B, Sq, H, D, device=q.device, dtype=q.dtype)
+        lse = torch.empty(B * H * Sq, device=q.device, dtype=torch.float32)
+        kl = kv_lens.to(torch.int32).contiguous() if kv_lens is not None else None
+        rc = k_.flash_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), lse.data_ptr(),
+                          _strides(q), _strides(k), _strides(v), _strides(out), _lib.ptr(kl),
+                          B, H, Sq, Sk, D, int(causal), float(scale), float(p), key,
+                          _lib.stream())
+        if rc != 0:
+            raise RuntimeError("flash_fwd failed (%d)" % rc)
+        _lib.maybe_sync()
+        ctx.causal, ctx.p, ctx.key, ctx.scale = causal, p, key, scale
+        ctx.packed = packed is not None
+        ctx.save_for_backward(q, k, v, out, lse, kl)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, out, lse, kl = ctx.saved_tensors
+        B, Sq, H, D = q.shape
+        Sk = k.shape[1]
+        dout = dout.contiguous()
+        if ctx.packed:
+            dqkv = torch.empty(B, Sq, H, 3, D, device=q.device, dtype=q.dtype)
+            dq, dk, dv = dqkv[:, :, :, 0], dqkv[:, :, :, 1], dqkv[:, :, :, 2]
+        else:
+            dq = torch.empty(B, Sq, H, D, device=q.device, dtype=q.dtype)
+            dk = torch.empty(B, Sk, H, D, device=q.device, dtype=q.dtype)
+            dv = torch.empty_like(dk)
+        delta = torch.empty(B * H * Sq, device=q.device, dtype=torch.float32)
+        rc = _lib.kernels().flash_bwd(
+            q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), dout.data_ptr(),
+            lse.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
+            _strides(q), _strides(k), _strides(v), _strides(out), _strides(dq), _strides(dk),
+            _lib.ptr(kl), B, H, Sq, Sk, D, int(ctx.causal), float(ctx.scale), float(ctx.p),
+            ctx.key, _lib.stream())
+        if rc != 0:
+            raise RuntimeError("flash_bwd failed (%d)" % rc)
+        _lib.maybe_sync()
+        if ctx.packed:
+            return None, None, None, dqkv, None, None, None, None, None
+        return dq, dk, dv, None, None, None, None, None, None
+
+
+class _PackedEntry(torch.autograd.Function):
+    """Routes the packed-QKV gradient back to the packed tensor."""
+
+    @staticmethod
+    def forward(ctx, qkv, causal, p, key, scale, kv_lens):
+        q, k, v = qkv[:, :, :, 0], qkv[:, :, :, 1], qkv[:, :, :, 2]
+        return _FlashAttn.forward(ctx, q, k, v, qkv, causal, p, key, scale, kv_lens)
+
+    @staticmethod
+    def backward(ctx, dout):
+        grads = _FlashAttn.backward(ctx, dout)
+        return grads[3], None, None, None, None, None
+
+
+def flash_attention(q, k, v, causal=True, dropout_p=0.0, key=0, scale=None, kv_lens=None):
+    """q: [B, Sq, H, D], k/v: [B, Sk, H, D] (strided views allowed)."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    if not q.is_cuda:
+        return attention_reference(q, k, v, causal, dropout_p, key, scale, kv_lens)
+    return _FlashAttn.apply(q, k, v, None, causal, float(dropout_p), key, scale, kv_lens)
+
+
+def flash_attention_qkvpacked(qkv, causal=True, dropout_p=0.0, key=0, scale=None, kv_lens=None):
+    """qkv: [B, S, H, 3, D] -> out [B, S, H, D]; gradient lands in one packed buffer."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(qkv.shape[-1])
+    if not qkv.is_cuda:
+        return attention_reference(qkv[:, :, :, 0], qkv[:, :, :, 1], qkv[:, :, :, 2], causal,
+                                   dropout_p, key, scale, kv_lens)
+    return _PackedEntry.apply(qkv, causal, float(dropout_p), key, scale, kv_lens)
+
+
+def decode_attention(q, k_cache, v_cache, lens, scale=None):
+    """Single-token attention over a KV cache.
+
+    q: [B, H, D]; caches: [B, maxlen, H, D]; lens: int32 [B] valid lengths.
+    """
+    B, H, D = q.shape
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if not q.is_cuda:
+        L = k_cache.shape[1]
+        s = torch.einsum("bhd,blhd->bhl", q.float(), k_cache.float()) * scale
+        m = torch.arange(L, device=q.device).view(1, 1, L) >= lens.view(B, 1, 1).to(q.device)
+        p = torch.softmax(s.masked_fill(m, float("-inf")), -1)
+        return torch.einsum("bhl,blhd->bhd", p, v_cache.float()).to(q.dtype)
+    out = torch.empty(B, H, D, device=q.device, dtype=q.dtype)
+    rc = _lib.kernels().decode_attn(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                                    out.data_ptr(), lens.to(torch.int32).contiguous().data_ptr(),
+                                    B, H, D, k_cache.shape[1], 1, q.stride(0), q.stride(1),
+                                    k_cache.stride(0), k_cache.stride(1), k_cache.stride(2),
+                                    out.stride(0), float(scale), _lib.stream())
+    if rc != 0:
+        raise NotImplementedError("decode attention supports head_dim 64/128")
+    return out

@@ -1,0 +1,160 @@
+"""Bias+GeLU, bias+dropout+residual-add and plain dropout.
+
+Reference K08 (``F.gelu(approximate=True)`` after FFN1; ViT uses exact GeLU)
+and K09 (``dropout(upscale_in_train)`` + residual).  The GEMM runs bias-free on
+hipBLASLt; these kernels carry the epilogue and emit dbias from the same
+pass as dx in backward.
+"""
+import math
+
+import torch
+
+from . import _lib
+from .norm import _dropout_ref, col_sum
+
+
+def _gelu_ref(x, erf):
+    if erf:
+        return 0.5 * x * (1.0 + torch.erf(x / math.sqrt(2.0)))
+    return 0.5 * x * (1.0 + torch.tanh(0.7978845608028654 * (x + 0.044715 * x ** 3)))
+
+
+def _gelu_grad_ref(x, erf):
+    if erf:
+        return 0.5 * (1.0 + torch.erf(x / math.sqrt(2.0))) + x * 0.3989422804014327 * torch.exp(-0.5 * x * x)
+    u = 0.7978845608028654 * (x + 0.044715 * x ** 3)
+    t = torch.tanh(u)
+    return 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * x * x)
+
+
+class _BiasGelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bias, erf):
+        ctx.erf = erf
+        ctx.has_bias = bias is not None
+        x = x.contiguous()
+        cols = x.shape[-1]
+        if x.is_cuda:
+            y = torch.empty_like(x)
+            _lib.kernels().bias_gelu_fwd(_lib.dt_code(x.dtype), int(erf), x.data_ptr(),
+                                         _lib.ptr(bias), y.data_ptr(), x.numel(), cols,
+                                         _lib.stream())
+        else:
+            t = x.float() + (bias.float() if bias is not None else 0.0)
+            y = _gelu_ref(t, erf).to(x.dtype)
+        ctx.save_for_backward(x, bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, bias = ctx.saved_tensors
+        dy = dy.contiguous()
+        cols = x.shape[-1]
+        rows = x.numel() // cols
+        if dy.is_cuda:
+            k = _lib.kernels()
+            splits = k.coltile_splits(rows, cols)
+            part = torch.empty(splits, cols, device=x.device, dtype=torch.float32)
+            dx = torch.empty_like(x)
+            dc = _lib.dt_code(x.dtype)
+            st = _lib.stream()
+            k.bias_gelu_bwd(dc, int(ctx.erf), dy.data_ptr(), x.data_ptr(), _lib.ptr(bias),
+                            dx.data_ptr(), part.data_ptr(), rows, cols, splits, st)
+            db = None
+            if ctx.has_bias:
+                db = torch.empty(cols, device=x.device, dtype=bias.dtype)
+                k.coltile_finalize(dc, part.data_ptr(), splits, cols, 0, db.data_ptr(), 0, st)
+        else:
+            t = x.float() + (bias.float() if bias is not None else 0.0)
+            dx = (dy.float() * _gelu_grad_ref(t, ctx.erf)).to(x.dtype)
+            db = dx.float().reshape(rows, cols).sum(0).to(bias.dtype) if ctx.has_bias else None
+        return dx, db, None
+
+
+def bias_gelu(x, bias=None, approximate=True):
+    return _BiasGelu.apply(x, bias, not approximate)
+
+
+class _BiasDropoutAdd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bias, residual, p, key):
+        ctx.p, ctx.key = p, key
+        ctx.has_bias, ctx.has_res = bias is not None, residual is not None
+        x = x.contiguous()
+        cols = x.shape[-1]
+        ctx.cols = cols
+        if x.is_cuda:
+            out = torch.empty_like(x)
+            if residual is not None:
+                residual = residual.contiguous()
+            _lib.kernels().bias_dropout_add_fwd(_lib.dt_code(x.dtype), x.data_ptr(),
+                                                _lib.ptr(bias), _lib.ptr(residual),
+                                                out.data_ptr(), x.numel(), cols, float(p), key,
+                                                _lib.stream())
+        else:
+            v = x if bias is None else x + bias
+            v = _dropout_ref(v, p, key)
+            out = v + residual if residual is not None else v
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        dout = dout.contiguous()
+        cols = ctx.cols
+        rows = dout.numel() // cols
+        dres = dout if ctx.has_res else None
+        if dout.is_cuda:
+            k = _lib.kernels()
+            dc = _lib.dt_code(dout.dtype)
+            st = _lib.stream()
+            dx = torch.empty_like(dout) if ctx.p > 0 else dout
+            db = None
+            if ctx.has_bias:
+                splits = k.coltile_splits(rows, cols)
+                part = torch.empty(splits, cols, device=dout.device, dtype=torch.float32)
+                k.dropout_bwd_colsum(dc, dout.data_ptr(), dx.data_ptr() if ctx.p > 0 else 0,
+                                     part.data_ptr(), rows, cols, splits, float(ctx.p), ctx.key, st)
+                db = torch.empty(cols, device=dout.device, dtype=dout.dtype)
+                k.coltile_finalize(dc, part.data_ptr(), splits, cols, 0, db.data_ptr(), 0, st)
+            elif ctx.p > 0:
+                k.dropout_fwd(dc, dout.data_ptr(), dx.data_ptr(), dout.numel(), float(ctx.p),
+                              ctx.key, st)
+        else:
+            dx = _dropout_ref(dout, ctx.p, ctx.key)
+            db = dx.float().reshape(rows, cols).sum(0).to(dout.dtype) if ctx.has_bias else None
+        return dx, db, dres, None, None
+
+
+def bias_dropout_add(x, bias, residual, p=0.0, key=0):
+    """``residual + dropout(x + bias)`` with a counter-hash mask."""
+    return _BiasDropoutAdd.apply(x, bias, residual, float(p), key)
+
+
+def _dropout_apply(x, p, key):
+    x = x.contiguous()
+    if x.is_cuda:
+        y = torch.empty_like(x)
+        _lib.kernels().dropout_fwd(_lib.dt_code(x.dtype), x.data_ptr(), y.data_ptr(),
+                                   x.numel(), float(p), key, _lib.stream())
+        return y
+    return _dropout_ref(x, p, key)
+
+
+class _Dropout(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, key):
+        ctx.p, ctx.key = p, key
+        return _dropout_apply(x, p, key)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _dropout_apply(dy, ctx.p, ctx.key), None, None
+
+
+def dropout(x, p, key):
+    if p <= 0.0:
+        return x
+    return _Dropout.apply(x, float(p), key)
+
+
+__all__ = ["bias_gelu", "bias_dropout_add", "dropout", "col_sum"]

@@ -1,0 +1,154 @@
+"""LayerNorm with optional fused residual + bias + dropout prologue.
+
+``add_layer_norm(x, bias, residual, w, b)`` returns ``(s, y)`` with
+``s = residual + dropout(x + bias)`` (the new residual stream) and
+``y = LayerNorm(s)``: the pre-LN transformer's "dropout + residual add,
+then LN2" in one HBM pass (reference K07 + K09,
+``single_model.py:393-394,412``).
+"""
+import torch
+
+from . import _lib
+from ..parallel import rng as _rng
+
+
+def _col_reduce_ln(dy, s, mean, rstd, cols, dtype):
+    k = _lib.kernels()
+    rows = dy.numel() // cols
+    splits = k.coltile_splits(rows, cols)
+    p0 = torch.empty(splits, cols, device=dy.device, dtype=torch.float32)
+    p1 = torch.empty_like(p0)
+    st = _lib.stream()
+    dc = _lib.dt_code(dtype)
+    k.coltile_partial(dc, 0, dy.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                      p0.data_ptr(), p1.data_ptr(), rows, cols, splits, st)
+    dg = torch.empty(cols, device=dy.device, dtype=dtype)
+    db = torch.empty(cols, device=dy.device, dtype=dtype)
+    k.coltile_finalize(dc, p0.data_ptr(), splits, cols, 0, dg.data_ptr(), 0, st)
+    k.coltile_finalize(dc, p1.data_ptr(), splits, cols, 0, db.data_ptr(), 0, st)
+    return dg, db
+
+
+def col_sum(x, cols):
+    """Column sum of a [rows, cols] 16-bit tensor (fp32 accumulation)."""
+    if not x.is_cuda:
+        return x.reshape(-1, cols).float().sum(0).to(x.dtype)
+    k = _lib.kernels()
+    rows = x.numel() // cols
+    splits = k.coltile_splits(rows, cols)
+    p0 = torch.empty(splits, cols, device=x.device, dtype=torch.float32)
+    st = _lib.stream()
+    dc = _lib.dt_code(x.dtype)
+    k.coltile_partial(dc, 1, x.data_ptr(), 0, 0, 0, p0.data_ptr(), 0, rows, cols, splits, st)
+    out = torch.empty(cols, device=x.device, dtype=x.dtype)
+    k.coltile_finalize(dc, p0.data_ptr(), splits, cols, 0, out.data_ptr(), 0, st)
+    return out
+
+
+def _dropout_ref(x, p, key):
+    if p <= 0.0:
+        return x
+    m = _rng.keep_mask(x.shape, p, key, x.device)
+    return torch.where(m, x * (1.0 / (1.0 - p)), torch.zeros_like(x))
+
+
+class _AddLayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bias, residual, weight, lnbias, eps, p, key, store_sum):
+        h = x.shape[-1]
+        rows = x.numel() // h
+        ctx.p, ctx.key, ctx.has_bias, ctx.has_res = p, key, bias is not None, residual is not None
+        ctx.h = h
+        if x.is_cuda:
+            k = _lib.kernels()
+            x = x.contiguous()
+            fused = store_sum or bias is not None or residual is not None or p > 0
+            s = torch.empty_like(x) if fused else None
+            y = torch.empty_like(x)
+            mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+            rstd = torch.empty_like(mean)
+            k.add_ln_fwd(_lib.dt_code(x.dtype), x.data_ptr(), _lib.ptr(bias), _lib.ptr(residual),
+                         weight.data_ptr(), lnbias.data_ptr(), _lib.ptr(s), y.data_ptr(),
+                         mean.data_ptr(), rstd.data_ptr(), rows, h, float(eps), float(p), key,
+                         _lib.stream())
+            s_saved = s if s is not None else x
+        else:
+            v = x if bias is None else x + bias
+            v = _dropout_ref(v, p, key)
+            if residual is not None:
+                v = v + residual
+            s_saved = v
+            s = v if (store_sum or bias is not None or residual is not None or p > 0) else None
+            vf = v.float()
+            mean = vf.mean(-1).reshape(-1)
+            var = ((vf - mean.view(*vf.shape[:-1], 1)) ** 2).mean(-1).reshape(-1)
+            rstd = torch.rsqrt(var + eps)
+            y = ((vf - mean.view(*vf.shape[:-1], 1)) * rstd.view(*vf.shape[:-1], 1) * weight.float()
+                 + lnbias.float()).to(x.dtype)
+        ctx.save_for_backward(s_saved, mean, rstd, weight)
+        ctx.return_sum = s is not None
+        if s is None:
+            return y
+        return s, y
+
+    @staticmethod
+    def backward(ctx, *grads):
+        if ctx.return_sum:
+            ds_in, dy = grads
+        else:
+            ds_in, dy = None, grads[0]
+        s, mean, rstd, weight = ctx.saved_tensors
+        h = ctx.h
+        rows = s.numel() // h
+        dy = dy.contiguous()
+        if ds_in is not None:
+            ds_in = ds_in.contiguous()
+        if dy.is_cuda:
+            k = _lib.kernels()
+            dc = _lib.dt_code(dy.dtype)
+            ds = torch.empty_like(dy)
+            dx = torch.empty_like(dy) if ctx.p > 0 else ds
+            k.ln_bwd_row(dc, dy.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                         weight.data_ptr(), _lib.ptr(ds_in), ds.data_ptr(), dx.data_ptr(), rows, h,
+                         float(ctx.p), ctx.key, _lib.stream())
+            dw, db = _col_reduce_ln(dy, s, mean, rstd, h, dy.dtype)
+            dbias = col_sum(dx, h) if ctx.has_bias else None
+        else:
+            sf = s.float().reshape(rows, h)
+            xh = (sf - mean.view(rows, 1)) * rstd.view(rows, 1)
+            g = dy.float().reshape(rows, h) * weight.float()
+            m1 = g.mean(-1, keepdim=True)
+            m2 = (g * xh).mean(-1, keepdim=True)
+            dsf = rstd.view(rows, 1) * (g - m1 - xh * m2)
+            if ds_in is not None:
+                dsf = dsf + ds_in.float().reshape(rows, h)
+            ds = dsf.to(dy.dtype).reshape(dy.shape)
+            dx = _dropout_ref(ds, ctx.p, ctx.key)
+            dw = (dy.float().reshape(rows, h) * xh).sum(0).to(weight.dtype)
+            db = dy.float().reshape(rows, h).sum(0).to(weight.dtype)
+            dbias = dx.float().reshape(rows, h).sum(0).to(dy.dtype) if ctx.has_bias else None
+        dres = ds if ctx.has_res else None
+        return dx, dbias, dres, dw, db, None, None, None, None
+
+
+def add_layer_norm(x, bias, residual, weight, lnbias, eps=1e-5, p=0.0, key=0):
+    """Returns ``(s, y)``: s = residual + dropout(x + bias), y = LN(s)."""
+    return _AddLayerNorm.apply(x, bias, residual, weight, lnbias, eps, p, key, True)
+
+
+def layer_norm(x, weight, bias, eps=1e-5):
+    return _AddLayerNorm.apply(x, None, None, weight, bias, eps, 0.0, 0, False)
+
+
+class FusedLayerNorm(torch.nn.Module):
+    """``nn.LayerNorm`` replacement routed through the HIP kernel."""
+
+    def __init__(self, hidden, eps=1e-5, dtype=None, device=None):
+        super().__init__()
+        self.weight = torch.nn.Parameter(torch.ones(hidden, dtype=dtype, device=device))
+        self.bias = torch.nn.Parameter(torch.zeros(hidden, dtype=dtype, device=device))
+        self.eps = eps
+        self.normalized_shape = (hidden,)
+
+    def forward(self, x):
+        return layer_norm(x, self.weight, self.bias, self.eps)

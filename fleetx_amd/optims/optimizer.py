@@ -1,0 +1,258 @@
+"""Optimizers over flat fp32 master buffers (multi-precision, fused).
+
+Parity: reference ``FusedAdamW`` (``optimizer.py:29-50``: AdamW with
+decoupled weight decay skipped for bias/norm params, ``multi_precision``
+fp32 master weights, optional tensor fusion), re-exported ``Adam``,
+``AdamW``, ``Momentum``; ``ClipGradByGlobalNorm`` (K13) and the GradScaler
+path (K14) as used by ``eager_engine.py:425-445``.
+
+MI355X design: the optimizer works on the ranges of a
+:class:`~fleetx_amd.parallel.grad_buffer.FlatParamGradBuffer` -- master, m
+and v are flat fp32 tensors, one HIP ``adamw_flat`` launch per range (a
+handful per step, never one per parameter).  The global grad-norm is a
+squared-sum kernel per range + (mp / pp / sharding) all-reduces of ONE float;
+the clip coefficient and the fp16 found-inf flag stay on the device, so a
+step never synchronises the host.
+"""
+import math
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _lib
+
+
+class ClipGradByGlobalNorm:
+    def __init__(self, clip_norm=1.0, **kw):
+        self.clip_norm = float(clip_norm)
+
+
+class ClipGradByNorm(ClipGradByGlobalNorm):
+    pass
+
+
+def _sumsq(t):
+    if t.is_cuda:
+        k = _lib.kernels()
+        blocks = k.sumsq_blocks(t.numel())
+        part = torch.empty(blocks, device=t.device, dtype=torch.float32)
+        k.sumsq_f32(t.data_ptr(), t.numel(), part.data_ptr(), blocks, _lib.stream())
+        return part.sum()
+    return (t.float() * t.float()).sum()
+
+
+class FlatOptimizer:
+    """Base: owns master/state for the owned ranges of a flat buffer."""
+
+    def __init__(self, learning_rate, buffer, grad_clip=None, weight_decay=0.0,
+                 multi_precision=True, check_group=None, pp_group=None, mp_group=None):
+        self._lr = learning_rate
+        self.buffer = buffer
+        self.grad_clip = grad_clip
+        self.weight_decay = float(weight_decay or 0.0)
+        self.ranges = buffer.owned_ranges()
+        self.mp_group = mp_group if mp_group is not None and mp_group.nranks > 1 else None
+        self.pp_group = pp_group if pp_group is not None and pp_group.nranks > 1 else None
+        self.step_count = 0
+        dev = buffer.device
+        self.master = [buffer.param_flat[s:e].float().clone() for s, e, _ in self.ranges]
+        self.found_inf = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.gscale = torch.ones(1, dtype=torch.float32, device=dev)
+        self.last_grad_norm = torch.zeros((), dtype=torch.float32, device=dev)
+        self.loss_scale = None  # set by the engine for fp16 (device tensor)
+
+    # ------------------------------------------------------------------ lr
+    def get_lr(self):
+        return self._lr() if callable(self._lr) else float(self._lr)
+
+    @property
+    def lr_scheduler(self):
+        return self._lr if hasattr(self._lr, "step") else None
+
+    # ------------------------------------------------------------------ grads
+    def grad_views(self):
+        g = self.buffer.grad_flat
+        return [g[s:e] for s, e, _ in self.ranges]
+
+    def compute_grad_norm(self):
+        """Global L2 norm over the data/model-parallel world (device scalar)."""
+        dev = self.buffer.device
+        dist_sq = torch.zeros((), dtype=torch.float32, device=dev)
+        rep_sq = torch.zeros((), dtype=torch.float32, device=dev)
+        for (s, e, c), g in zip(self.ranges, self.grad_views()):
+            if c.norm_excluded:
+                continue
+            sq = _sumsq(g)
+            if c.distributed:
+                dist_sq = dist_sq + sq
+            else:
+                rep_sq = rep_sq + sq
+        shard = self.buffer.shard_group if self.buffer.shard_stage >= 1 else None
+        if shard is not None:
+            pair = torch.stack([dist_sq, rep_sq])
+            dist.all_reduce(pair, group=shard.group)
+            dist_sq, rep_sq = pair[0], pair[1]
+        if self.mp_group is not None:
+            dist.all_reduce(dist_sq, group=self.mp_group.group)
+        total = dist_sq + rep_sq
+        if self.pp_group is not None:
+            dist.all_reduce(total, group=self.pp_group.group)
+        return torch.sqrt(total)
+
+    def _prepare_scale(self):
+        """Device-side clip coefficient x loss-scale unscale, and found-inf."""
+        need_norm = self.grad_clip is not None or self.loss_scale is not None
+        if not need_norm:
+            self.gscale.fill_(1.0)
+            self.found_inf.zero_()
+            return
+        norm = self.compute_grad_norm()
+        inv_scale = 1.0 / self.loss_scale if self.loss_scale is not None else 1.0
+        true_norm = norm * inv_scale
+        self.last_grad_norm = true_norm.detach()
+        coef = torch.ones((), dtype=torch.float32, device=norm.device)
+        if self.grad_clip is not None:
+            coef = torch.clamp(self.grad_clip.clip_norm / (true_norm + 1e-6), max=1.0)
+        self.gscale.copy_((coef * inv_scale).reshape(1))
+        self.found_inf.copy_((~torch.isfinite(norm)).to(torch.int32).reshape(1))
+
+    # ------------------------------------------------------------------ API
+    def step(self):
+        self._prepare_scale()
+        self.step_count += 1
+        self._update(self.get_lr())
+        self.buffer.allgather_params()
+
+    def clear_grad(self, set_to_zero=True):
+        self.buffer.zero_grad()
+
+    zero_grad = clear_grad
+
+    def _update(self, lr):
+        raise NotImplementedError
+
+    def state_dict(self):
+        raise NotImplementedError
+
+    def set_state_dict(self, state):
+        raise NotImplementedError
+
+    def refresh_master_from_params(self):
+        for (s, e, _), m in zip(self.ranges, self.master):
+            m.copy_(self.buffer.param_flat[s:e].float())
+
+
+class FusedAdamW(FlatOptimizer):
+    """AdamW (decoupled decay) with fp32 master weights, one launch per range."""
+
+    decoupled = True
+
+    def __init__(self, learning_rate, buffer, grad_clip=None, weight_decay=0.01, beta1=0.9,
+                 beta2=0.999, epsilon=1e-8, multi_precision=True, **kw):
+        tensor_fusion = kw.pop("tensor_fusion", None)  # always fused here
+        del tensor_fusion
+        super().__init__(learning_rate, buffer, grad_clip, weight_decay, multi_precision,
+                         kw.get("check_group"), kw.get("pp_group"), kw.get("mp_group"))
+        self.beta1, self.beta2, self.eps = float(beta1), float(beta2), float(epsilon)
+        self.m = [torch.zeros_like(x) for x in self.master]
+        self.v = [torch.zeros_like(x) for x in self.master]
+
+    def _update(self, lr):
+        t = self.step_count
+        bc1 = 1.0 - self.beta1 ** t
+        bc2 = 1.0 - self.beta2 ** t
+        pf = self.buffer.param_flat
+        for (s, e, c), g, p, m, v in zip(self.ranges, self.grad_views(), self.master, self.m,
+                                         self.v):
+            wd = self.weight_decay if c.decay else 0.0
+            if not self.decoupled and wd:
+                g = g + wd * p
+                wd_eff = 0.0
+            else:
+                wd_eff = wd
+            out16 = pf[s:e]
+            if p.is_cuda:
+                _lib.kernels().adamw_flat(_lib.dt_code(pf.dtype), p.data_ptr(), g.data_ptr(),
+                                          m.data_ptr(), v.data_ptr(), out16.data_ptr(), p.numel(),
+                                          float(lr), self.beta1, self.beta2, self.eps,
+                                          float(wd_eff), bc1, bc2, self.gscale.data_ptr(),
+                                          self.found_inf.data_ptr(), _lib.stream())
+            else:
+                if int(self.found_inf.item()):
+                    continue
+                gg = g * self.gscale
+                m.mul_(self.beta1).add_(gg, alpha=1 - self.beta1)
+                v.mul_(self.beta2).addcmul_(gg, gg, value=1 - self.beta2)
+                denom = v.sqrt() / math.sqrt(bc2) + self.eps
+                p.mul_(1 - lr * wd_eff).addcdiv_(m, denom, value=-lr / bc1)
+                out16.copy_(p)
+
+    def state_dict(self):
+        return {"step": self.step_count, "master": [x.cpu() for x in self.master],
+                "m": [x.cpu() for x in self.m], "v": [x.cpu() for x in self.v],
+                "lr": self._lr.state_dict() if hasattr(self._lr, "state_dict") else self._lr}
+
+    def set_state_dict(self, state):
+        self.step_count = state["step"]
+        for dst, src in zip(self.master, state["master"]):
+            dst.copy_(src)
+        for dst, src in zip(self.m, state["m"]):
+            dst.copy_(src)
+        for dst, src in zip(self.v, state["v"]):
+            dst.copy_(src)
+        if hasattr(self._lr, "set_state_dict") and isinstance(state.get("lr"), dict):
+            self._lr.set_state_dict(state["lr"])
+        pf = self.buffer.param_flat
+        for (s, e, _), p in zip(self.ranges, self.master):
+            pf[s:e].copy_(p)
+
+
+class AdamW(FusedAdamW):
+    pass
+
+
+class Adam(FusedAdamW):
+    """Adam with classic (L2) weight decay added to the gradient."""
+    decoupled = False
+
+
+class Momentum(FlatOptimizer):
+    def __init__(self, learning_rate, buffer, grad_clip=None, momentum=0.9, weight_decay=0.0,
+                 use_nesterov=False, multi_precision=True, **kw):
+        super().__init__(learning_rate, buffer, grad_clip, weight_decay, multi_precision,
+                         kw.get("check_group"), kw.get("pp_group"), kw.get("mp_group"))
+        self.momentum = float(momentum)
+        self.nesterov = use_nesterov
+        self.vel = [torch.zeros_like(x) for x in self.master]
+
+    def _update(self, lr):
+        skip = bool(self.found_inf.item()) if self.loss_scale is not None else False
+        if skip:
+            return
+        pf = self.buffer.param_flat
+        for (s, e, c), g, p, vel in zip(self.ranges, self.grad_views(), self.master, self.vel):
+            gg = g * self.gscale
+            if c.decay and self.weight_decay:
+                gg = gg + self.weight_decay * p
+            vel.mul_(self.momentum).add_(gg)
+            upd = gg + self.momentum * vel if self.nesterov else vel
+            p.add_(upd, alpha=-lr)
+            pf[s:e].copy_(p)
+
+    def state_dict(self):
+        return {"step": self.step_count, "master": [x.cpu() for x in self.master],
+                "vel": [x.cpu() for x in self.vel]}
+
+    def set_state_dict(self, state):
+        self.step_count = state["step"]
+        for dst, src in zip(self.master, state["master"]):
+            dst.copy_(src)
+        for dst, src in zip(self.vel, state["vel"]):
+            dst.copy_(src)
+        pf = self.buffer.param_flat
+        for (s, e, _), p in zip(self.ranges, self.master):
+            pf[s:e].copy_(p)
+
+
+OPTIMIZERS = {"FusedAdamW": FusedAdamW, "AdamW": AdamW, "Adam": Adam, "Momentum": Momentum}
+CLIPS = {"ClipGradByGlobalNorm": ClipGradByGlobalNorm, "ClipGradByNorm": ClipGradByNorm}

@@ -1,0 +1,287 @@
+"""Flat parameter / gradient storage with bucketed, backward-overlapped
+RCCL gradient reduction (data parallel + ZeRO stage 1/2 sharding).
+
+Capability parity:
+* P09 tensor fusion (``tensor_fusion_helper.py:36-127``: 256-byte aligned
+  flat ``ParamStorage/GradStorage``, decay / no-decay split);
+* P02 data parallel (Paddle ``DataParallel`` reducer: bucketed all-reduce
+  overlapped with backward, ``fused_allreduce_gradients``);
+* P06 sharding stage 1/2 gradient path (reduce-scatter to the owning rank);
+* N09 coalesced mp all-reduce of sequence-parallel replicated grads;
+* N11 tied-embedding grad all-reduce between first and last pipeline stage.
+
+MI355X design:
+* every trainable parameter becomes a VIEW into one model-dtype flat buffer
+  and owns a ``main_grad`` view into one fp32 flat buffer; autograd's bf16
+  ``.grad`` is folded into ``main_grad`` by a post-accumulate hook and freed,
+  so gradient accumulation across micro-batches is exact fp32;
+* parameters are grouped by category (weight-decay, tensor-parallel
+  distributed, sequence-parallel, norm-excluded) so the optimizer, the grad
+  norm and the SP all-reduce each see a handful of contiguous ranges (one
+  kernel / one RCCL call per range, never per tensor);
+* inside a category, parameters are laid out in reverse registration order
+  (~ backward order) and cut into buckets of ``bucket_mb`` (default 256 MiB:
+  few, large RCCL calls -- on xGMI a ring is per-link bandwidth bound, so a
+  bucket must be large enough to amortise the ~10-20 us RCCL launch and
+  protocol latency); a bucket's collective is launched asynchronously the
+  moment its last gradient lands during the LAST micro-batch's backward, so
+  communication overlaps the rest of backward on RCCL's stream.
+"""
+import math
+
+import torch
+import torch.distributed as dist
+
+ALIGN = 128  # elements (256 B in bf16, 512 B in fp32)
+
+
+def _round_up(n, a):
+    return (n + a - 1) // a * a
+
+
+class Category:
+    __slots__ = ("key", "start", "end", "params")
+
+    def __init__(self, key):
+        self.key = key
+        self.start = self.end = 0
+        self.params = []
+
+    @property
+    def decay(self):
+        return self.key[0]
+
+    @property
+    def distributed(self):
+        return self.key[1]
+
+    @property
+    def seq_parallel(self):
+        return self.key[2]
+
+    @property
+    def norm_excluded(self):
+        return self.key[3]
+
+
+class Bucket:
+    __slots__ = ("start", "end", "params", "ready", "work", "launched", "shard_ranges")
+
+    def __init__(self, start, end, params):
+        self.start, self.end, self.params = start, end, params
+        self.ready = 0
+        self.work = None
+        self.launched = False
+
+
+def default_decay_fn(name, p):
+    """Reference rule: no decay for biases and norm params (``optimizer.py:39-43``)."""
+    if p.ndim < 2:
+        return False
+    return not any(nd in name for nd in ("bias", "norm"))
+
+
+class FlatParamGradBuffer:
+    """Owns flat param / fp32 grad storage and the gradient synchronisation."""
+
+    def __init__(self, named_params, dp_group=None, shard_group=None, mp_group=None,
+                 embed_group=None, bucket_mb=256, overlap=True, shard_stage=0,
+                 decay_fn=default_decay_fn, reduce_dtype=torch.float32):
+        named = [(n, p) for n, p in named_params if p.requires_grad]
+        assert named, "no trainable parameters"
+        self.dtype = named[0][1].dtype
+        self.device = named[0][1].device
+        self.dp_group = dp_group if dp_group is not None and dp_group.nranks > 1 else None
+        self.shard_group = shard_group if shard_group is not None and shard_group.nranks > 1 else None
+        self.mp_group = mp_group if mp_group is not None and mp_group.nranks > 1 else None
+        self.embed_group = embed_group if embed_group is not None and embed_group.nranks > 1 else None
+        self.shard_stage = shard_stage if self.shard_group is not None else 0
+        self.overlap = overlap
+        self.reduce_dtype = reduce_dtype
+
+        cats = {}
+        for n, p in reversed(named):
+            key = (bool(decay_fn(n, p)), bool(getattr(p, "is_distributed", False)),
+                   bool(getattr(p, "sequence_parallel", False)),
+                   bool(getattr(p, "norm_exclude", False)))
+            cats.setdefault(key, Category(key)).params.append((n, p))
+        # deterministic category order: big decay/distributed region first
+        order = sorted(cats.keys(), key=lambda k: (not k[0], not k[1], k[2], k[3]))
+        self.categories = [cats[k] for k in order]
+
+        # shard padding: each category region is a multiple of ALIGN * nshard
+        nsh = self.shard_group.nranks if self.shard_group is not None else 1
+        off = 0
+        self.offsets = {}
+        for c in self.categories:
+            c.start = off
+            for n, p in c.params:
+                self.offsets[id(p)] = (off, p.numel())
+                off += _round_up(p.numel(), ALIGN)
+            off = _round_up(off, ALIGN * nsh)
+            c.end = off
+        self.numel = off
+        self.param_flat = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
+        self.grad_flat = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        self.params = []
+        for c in self.categories:
+            for n, p in c.params:
+                o, k = self.offsets[id(p)]
+                view = self.param_flat[o:o + k].view_as(p)
+                view.copy_(p.data)
+                p.data = view
+                p.main_grad = self.grad_flat[o:o + k].view_as(p)
+                p.grad = None
+                self.params.append((n, p))
+
+        # buckets: contiguous slices inside a category, capped at bucket_mb
+        cap = max(ALIGN, int(bucket_mb * 1024 * 1024 // 4))
+        self.buckets = []
+        self._bucket_of = {}
+        for c in self.categories:
+            cur, cur_start, fill = [], c.start, 0
+            for n, p in c.params:
+                o, k = self.offsets[id(p)]
+                if cur and fill + k > cap:
+                    self._add_bucket(cur_start, o, cur)
+                    cur, cur_start, fill = [], o, 0
+                cur.append(p)
+                fill += _round_up(k, ALIGN)
+            if cur:
+                self._add_bucket(cur_start, c.end, cur)
+        if nsh > 1:
+            for b in self.buckets:
+                assert (b.end - b.start) % nsh == 0
+        self._hooks = []
+        self._accumulating = True
+        self._last_micro = True
+        self._install_hooks()
+
+    # ------------------------------------------------------------------ setup
+    def _add_bucket(self, start, end, params):
+        nsh = self.shard_group.nranks if self.shard_group is not None else 1
+        # pad bucket end so it splits evenly over sharding ranks (ranges are ALIGN aligned)
+        b = Bucket(start, end, params)
+        if nsh > 1 and (end - start) % nsh:
+            raise RuntimeError("bucket not divisible by sharding degree")
+        self.buckets.append(b)
+        for p in params:
+            self._bucket_of[id(p)] = b
+
+    def _install_hooks(self):
+        for n, p in self.params:
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(p)))
+
+    def _make_hook(self, p):
+        def hook(param):
+            g = param.grad
+            if g is not None:
+                param.main_grad.add_(g)
+                param.grad = None
+            b = self._bucket_of[id(param)]
+            b.ready += 1
+            if b.ready == len(b.params) and self._last_micro and self.overlap:
+                self._launch(b)
+        return hook
+
+    # ------------------------------------------------------------------ control
+    def set_last_micro_batch(self, last):
+        """Only the last micro-batch's backward launches the reductions."""
+        self._last_micro = last
+        for b in self.buckets:
+            b.ready = 0
+
+    def zero_grad(self):
+        self.grad_flat.zero_()
+        for b in self.buckets:
+            b.ready = 0
+            b.work = None
+            b.launched = False
+
+    def _data_groups(self):
+        return self.dp_group, self.shard_group
+
+    def _launch(self, b):
+        if b.launched:
+            return
+        b.launched = True
+        seg = self.grad_flat[b.start:b.end]
+        works = []
+        if self.shard_stage >= 1 and self.shard_group is not None:
+            # reduce-scatter to the owner; dp all-reduce of the owned shard
+            n = self.shard_group.nranks
+            r = self.shard_group.rank
+            chunk = (b.end - b.start) // n
+            out = self.grad_flat[b.start + r * chunk:b.start + (r + 1) * chunk]
+            works.append(dist.reduce_scatter_tensor(out, seg, group=self.shard_group.group,
+                                                    async_op=True))
+            b.work = ("rs", works, out)
+        else:
+            grp = self.dp_group
+            if grp is not None:
+                works.append(dist.all_reduce(seg, group=grp.group, async_op=True))
+            b.work = ("ar", works, seg)
+
+    def finish(self):
+        """Complete every gradient collective; average over the data world."""
+        for b in self.buckets:
+            if not b.launched:
+                self._launch(b)
+        data_world = 1
+        if self.dp_group is not None:
+            data_world *= self.dp_group.nranks
+        if self.shard_group is not None:
+            data_world *= self.shard_group.nranks
+        for b in self.buckets:
+            kind, works, seg = b.work
+            for w in works:
+                w.wait()
+            if kind == "rs" and self.dp_group is not None:
+                dist.all_reduce(seg, group=self.dp_group.group)
+            if data_world > 1:
+                seg.mul_(1.0 / data_world)
+        # sequence-parallel replicated params: one coalesced mp all-reduce per range
+        if self.mp_group is not None:
+            for c in self.categories:
+                if c.seq_parallel:
+                    dist.all_reduce(self.grad_flat[c.start:c.end], group=self.mp_group.group)
+        # tied embedding between first and last pipeline stage
+        if self.embed_group is not None:
+            for n, p in self.params:
+                if getattr(p, "shared_embedding", False):
+                    dist.all_reduce(p.main_grad, group=self.embed_group.group)
+        for b in self.buckets:
+            b.launched = False
+            b.work = None
+            b.ready = 0
+
+    # ------------------------------------------------------------------ sharding views
+    def owned_ranges(self):
+        """(start, end, category) ranges whose optimizer state this rank owns."""
+        if self.shard_stage < 1 or self.shard_group is None:
+            return [(c.start, c.end, c) for c in self.categories]
+        n, r = self.shard_group.nranks, self.shard_group.rank
+        out = []
+        for c in self.categories:
+            for b in self.buckets:
+                if b.start >= c.start and b.end <= c.end:
+                    chunk = (b.end - b.start) // n
+                    out.append((b.start + r * chunk, b.start + (r + 1) * chunk, c))
+        return out
+
+    def allgather_params(self):
+        """After a sharded update, every rank gathers the full model-dtype params."""
+        if self.shard_stage < 1 or self.shard_group is None:
+            return
+        n = self.shard_group.nranks
+        r = self.shard_group.rank
+        for b in self.buckets:
+            chunk = (b.end - b.start) // n
+            full = self.param_flat[b.start:b.end]
+            mine = full[r * chunk:(r + 1) * chunk].clone()
+            dist.all_gather_into_tensor(full, mine, group=self.shard_group.group)
+
+    def remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

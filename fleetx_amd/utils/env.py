@@ -1,0 +1,64 @@
+"""Process environment: seeding, distributed init, data-world geometry.
+
+Parity: reference ``ppfleetx/utils/env.py:27-96`` (``set_seed``,
+``init_dist_env``, ``get_local_rank``, ``get_data_world_size/rank``).
+"""
+import os
+import random
+
+import numpy as np
+import torch
+
+from ..parallel import topology as topo
+from ..parallel.rng import model_parallel_random_seed
+
+
+def get_local_rank():
+    return int(os.environ.get("LOCAL_RANK", os.environ.get("PADDLE_RANK_IN_NODE", "0")))
+
+
+def get_rank():
+    return int(os.environ.get("RANK", "0"))
+
+
+def get_world_size():
+    return int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def init_dist_env(config, backend=None):
+    """Create the process group and the hybrid topology from ``Distributed``."""
+    d = config.Distributed
+    topo.init_distributed(backend=backend)
+    hcg = topo.init_hcg(dp=d.dp_degree, mp=d.mp_degree, pp=d.pp_degree,
+                        sharding=d.sharding.sharding_degree)
+    return hcg
+
+
+def get_data_world_size():
+    hcg = topo.get_hcg()
+    return hcg.dp_degree * hcg.sharding_degree
+
+
+def get_data_world_rank():
+    hcg = topo.get_hcg()
+    return hcg.dp_rank * hcg.sharding_degree + hcg.sharding_rank
+
+
+def set_seed(seed):
+    """Seed host RNGs with ``seed + data_rank`` and the dropout tracker."""
+    hcg = topo.get_hcg()
+    data_rank = get_data_world_rank()
+    s = seed + data_rank
+    random.seed(s)
+    np.random.seed(s % (2 ** 32))
+    torch.manual_seed(s)
+    model_parallel_random_seed(seed, mp_rank=hcg.mp_rank, pp_rank=hcg.pp_rank,
+                               data_rank=data_rank)
+    # parameter-init seed for mp-sharded weights (reference env.py:67)
+    return s
+
+
+def device():
+    if torch.cuda.is_available():
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
