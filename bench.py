@@ -1,0 +1,167 @@
+"""Headline benchmark: GPT-3 6.7B pretraining tokens/s (whole job) on MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
+it is launched by ``torch.distributed.run`` (one rank per GPU, RCCL).  W
+untimed warmup steps, then exactly K full training steps (forward, backward,
+gradient reduction, global-norm clip, AdamW update, LR step) bracketed by a
+barrier + device synchronize; the elapsed time is the MAX over ranks; rank 0
+prints one JSON line.
+
+Config = BASELINE.json metric "tokens/sec (whole node) GPT-3 6.7B
+hybrid-parallel at 1/2/4/8 MI355X": h 4096, 32 layers, 32 heads, vocab
+50304, seq 1024, dropout 0.1 (as ``pretrain_gpt_6.7B_sharding16.yaml``), bf16
+compute with fp32 master weights, synthetic tokens, random-init weights.
+Layouts follow BASELINE.md: 1 GPU dp1, 2 tp2, 4 tp2*pp2, 8 tp2*pp2*dp2 (1F1B),
+weak scaling: 8 sequences x 1024 tokens of work per GPU per step.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+MODELS = {
+    # name: (hidden, layers, heads)
+    "gpt3-6.7B": (4096, 32, 32),
+    "gpt3-1.3B": (2048, 24, 16),
+    "gpt-345M": (1024, 24, 16),
+    "gpt-tiny": (256, 2, 4),
+}
+PEAK_BF16 = 2.5e15  # MI355X dense bf16 (spec), per GPU
+
+# per-GPU count -> (dp, mp, pp, micro_batch)
+LAYOUTS = {1: (1, 1, 1, 8), 2: (1, 2, 1, 8), 4: (1, 2, 2, 2), 8: (2, 2, 2, 2)}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="gpt3-6.7B", choices=sorted(MODELS))
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--per-gpu-seqs", type=int, default=8,
+                    help="sequences of work per GPU per step (weak scaling)")
+    ap.add_argument("--layout", default=None, help="dp,mp,pp,micro override, e.g. 8,1,1,8")
+    ap.add_argument("--recompute", action="store_true")
+    ap.add_argument("--sequence-parallel", action="store_true")
+    ap.add_argument("--no-dropout", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from fleetx_amd.utils import config as cfgmod
+    from fleetx_amd.utils import env
+    from fleetx_amd.models import build_module
+    from fleetx_amd.core.engine.eager_engine import EagerEngine
+    from fleetx_amd.models.language_model.gpt.model import flops_per_token
+    from fleetx_amd.utils.log import logger
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    n = world
+    if args.gpus != world:
+        if world == 1 and args.gpus > 1:
+            print("bench.py --gpus %d must be launched with torch.distributed.run" % args.gpus,
+                  file=sys.stderr)
+            sys.exit(2)
+    if args.layout:
+        dp, mp, pp, micro = [int(x) for x in args.layout.split(",")]
+    else:
+        dp, mp, pp, micro = LAYOUTS.get(n, (n, 1, 1, 8))
+    assert dp * mp * pp == n, "layout {} does not match {} GPUs".format((dp, mp, pp), n)
+    h, L, a = MODELS[args.model]
+    global_batch = args.per_gpu_seqs * n
+    local_batch = global_batch // dp
+    micro = min(micro, local_batch)
+    drop = 0.0 if args.no_dropout else 0.1
+    here = os.path.dirname(os.path.abspath(__file__))
+    cfg_file = os.path.join(here, "fleetx_amd/configs/nlp/gpt/pretrain_gpt_345M_single_card.yaml")
+    ov = ["Model.hidden_size=%d" % h, "Model.num_layers=%d" % L,
+          "Model.num_attention_heads=%d" % a, "Model.vocab_size=50304",
+          "Model.hidden_dropout_prob=%s" % drop, "Model.attention_probs_dropout_prob=%s" % drop,
+          "Model.max_position_embeddings=%d" % max(1024, args.seq),
+          "Model.use_recompute=%s" % bool(args.recompute),
+          "Model.sequence_parallel=%s" % bool(args.sequence_parallel),
+          "Global.local_batch_size=%d" % local_batch, "Global.micro_batch_size=%d" % micro,
+          "Global.global_batch_size=None",
+          "Distributed.dp_degree=%d" % dp, "Distributed.mp_degree=%d" % mp,
+          "Distributed.pp_degree=%d" % pp,
+          "Engine.max_steps=%d" % (args.steps + args.warmup), "Engine.logging_freq=1000000",
+          "Engine.save_load.save_steps=-1", "Engine.mix_precision.dtype=bfloat16",
+          "Data.Train.dataset.max_seq_len=%d" % args.seq,
+          "Data.Train.dataset.name=SyntheticGPTDataset"]
+    os.environ.setdefault("FLEETX_LOG_RANK0_ONLY", "1")
+    cfg = cfgmod.get_config(cfg_file, overrides=ov, nranks=n)
+    env.init_dist_env(cfg)
+    env.set_seed(cfg.Global.seed)
+    module = build_module(cfg)
+    engine = EagerEngine(configs=cfg, module=module, mode="train")
+    dev = engine.device
+    hcg = engine.hcg
+    V = cfg.Model.vocab_size
+    S = args.seq
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + hcg.dp_rank)
+
+    def batch():
+        toks = torch.randint(0, V, (local_batch, S + 1), device=dev, generator=gen)
+        pos = torch.arange(S, device=dev).unsqueeze(0).expand(local_batch, S)
+        return [toks[:, :-1].contiguous(), pos, toks[:, 1:].contiguous(),
+                torch.ones(local_batch, S, device=dev)]
+
+    def step():
+        return engine._fit_impl(batch())
+
+    for _ in range(args.warmup):
+        loss = step()
+    sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
+    sync()
+    if dist.is_initialized():
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    sync()
+    if dist.is_initialized():
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if dist.is_initialized():
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    lval = engine._reduce_log_loss(loss, 1)
+    tokens = global_batch * S * args.steps
+    tps = tokens / elapsed
+    fpt = flops_per_token(module.gpt_config, S)
+    mfu = tps * fpt / (n * PEAK_BF16)
+    if env.get_rank() == 0:
+        out = {
+            "metric": "tokens/sec (whole node) GPT-3 6.7B hybrid-parallel at 1/2/4/8 MI355X"
+            if args.model == "gpt3-6.7B" else "tokens/sec %s" % args.model,
+            "value": round(tps, 1), "unit": "tokens/s", "n_gpus": n, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if engine._dtype == torch.bfloat16 else str(engine._dtype).replace("torch.", ""), "data": "synthetic (random tokens), random-init weights",
+            "config": {"model": args.model, "global_batch": global_batch, "seq_len": S,
+                       "parallelism": "dp%d_tp%d_pp%d" % (dp, mp, pp), "micro_batch": micro,
+                       "dropout": drop, "recompute": bool(args.recompute)},
+            "mfu": round(mfu, 4), "tokens_per_gpu": round(tps / n, 1),
+            "final_loss": round(lval, 4),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)
+            if torch.cuda.is_available() else None,
+        }
+        print(json.dumps(out), flush=True)
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

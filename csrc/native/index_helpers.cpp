@@ -12,6 +12,7 @@
 // the heavy loops, and result buffers handed to numpy without copies.
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include <algorithm>
 #include <cstdint>

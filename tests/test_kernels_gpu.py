@@ -1,0 +1,269 @@
+"""HIP kernel numerics vs plain PyTorch fp32 references (MI355X only)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from fleetx_amd.ops import _lib
+    _lib.kernels()  # fail loudly if the extension is missing
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.fixture(autouse=True)
+def _gpu():
+    _need_gpu()
+    torch.manual_seed(0)
+
+
+# ---------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("h", [1024, 4096, 2560])
+@pytest.mark.parametrize("fused", [False, True])
+def test_layer_norm_fwd_bwd(h, fused):
+    from fleetx_amd import ops
+    from fleetx_amd.parallel import rng
+    rows = 512
+    x = torch.randn(rows, h, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(h, device=DEV)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(h, device=DEV)).bfloat16().requires_grad_()
+    p, key = (0.1, 987654321) if fused else (0.0, 0)
+    if fused:
+        bias = (0.1 * torch.randn(h, device=DEV)).bfloat16().requires_grad_()
+        res = torch.randn(rows, h, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+        s, y = ops.add_layer_norm(x, bias, res, w, b, 1e-5, p, key)
+    else:
+        y = ops.layer_norm(x, w, b, 1e-5)
+    # fp32 reference (same dropout mask from the shared counter hash)
+    xr = x.detach().float().requires_grad_()
+    wr, br = w.detach().float().requires_grad_(), b.detach().float().requires_grad_()
+    if fused:
+        biasr = bias.detach().float().requires_grad_()
+        resr = res.detach().float().requires_grad_()
+        keep = rng.keep_mask((rows, h), p, key, DEV)
+        v = torch.where(keep, (xr + biasr) / (1 - p), torch.zeros_like(xr)) + resr
+        sr = v
+    else:
+        v = xr
+    yr = torch.nn.functional.layer_norm(v, (h,), wr, br, 1e-5)
+    assert _rel(y, yr) < 1e-2
+    if fused:
+        assert _rel(s, sr) < 1e-2
+    gy = torch.randn_like(yr)
+    loss = (y.float() * gy).sum() + ((s.float() * gy).sum() if fused else 0)
+    loss.backward()
+    lr_ = (yr * gy).sum() + ((sr * gy).sum() if fused else 0)
+    lr_.backward()
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(w.grad, wr.grad) < 2e-2
+    assert _rel(b.grad, br.grad) < 2e-2
+    if fused:
+        assert _rel(bias.grad, biasr.grad) < 2e-2
+        assert _rel(res.grad, resr.grad) < 2e-2
+
+
+# ---------------------------------------------------------------- GeLU / dropout
+@pytest.mark.parametrize("approx", [True, False])
+def test_bias_gelu(approx):
+    from fleetx_amd import ops
+    x = torch.randn(300, 2048, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    b = (0.1 * torch.randn(2048, device=DEV)).bfloat16().requires_grad_()
+    y = ops.bias_gelu(x, b, approximate=approx)
+    xr, br = x.detach().float().requires_grad_(), b.detach().float().requires_grad_()
+    yr = torch.nn.functional.gelu(xr + br, approximate="tanh" if approx else "none")
+    assert _rel(y, yr) < 1e-2
+    g = torch.randn_like(yr)
+    (y.float() * g).sum().backward()
+    (yr * g).sum().backward()
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(b.grad, br.grad) < 2e-2
+
+
+def test_bias_dropout_add_matches_cpu_mask():
+    from fleetx_amd import ops
+    x = torch.randn(64, 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    b = torch.randn(1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn(64, 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    out = ops.bias_dropout_add(x, b, r, 0.1, 42)
+    out_cpu = ops.bias_dropout_add(x.detach().cpu().float(), b.detach().cpu().float(),
+                                   r.detach().cpu().float(), 0.1, 42)
+    assert _rel(out.cpu(), out_cpu) < 1e-2
+    keep_frac = ((out.float() - r.float()) != 0).float().mean().item()
+    assert 0.88 < keep_frac < 0.92
+    g = torch.randn_like(out)
+    out.backward(g)
+    xr = x.detach().cpu().float().requires_grad_()
+    br = b.detach().cpu().float().requires_grad_()
+    o2 = ops.bias_dropout_add(xr, br, r.detach().cpu().float(), 0.1, 42)
+    o2.backward(g.cpu().float())
+    assert _rel(x.grad.cpu(), xr.grad) < 1e-2
+    assert _rel(b.grad.cpu(), br.grad) < 1e-2
+    assert torch.equal(r.grad, g)
+
+
+# ---------------------------------------------------------------- CE / embedding
+def test_cross_entropy():
+    from fleetx_amd import ops
+    V = 50304
+    logits = (3 * torch.randn(256, V, device=DEV)).bfloat16().requires_grad_()
+    labels = torch.randint(0, V, (256,), device=DEV)
+    ref_in = logits.detach().float().requires_grad_()
+    loss = ops.softmax_cross_entropy(logits.clone(), labels)
+    lr_ = torch.nn.functional.cross_entropy(ref_in, labels, reduction="none")
+    assert torch.allclose(loss, lr_, atol=2e-3, rtol=1e-3)
+    lg = logits.detach().clone().requires_grad_()
+    l2 = ops.softmax_cross_entropy(lg, labels, inplace_backward=False)
+    g = torch.rand(256, device=DEV)
+    (l2 * g).sum().backward()
+    (lr_ * g).sum().backward()
+    assert _rel(lg.grad, ref_in.grad) < 1e-2
+
+
+def test_embedding():
+    from fleetx_amd import ops
+    V, h = 1000, 512
+    W = torch.randn(V, h, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    P = torch.randn(128, h, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    ids = torch.randint(0, V, (4, 128), device=DEV)
+    pos = torch.arange(128, device=DEV).expand(4, 128)
+    out = ops.embedding(ids, W, pos, P)
+    ref = W.detach().float()[ids] + P.detach().float()[pos]
+    assert _rel(out, ref) < 1e-2
+    g = torch.randn_like(out)
+    out.backward(g)
+    Wr, Pr = W.detach().float().requires_grad_(), P.detach().float().requires_grad_()
+    (torch.nn.functional.embedding(ids, Wr) + Pr[pos]).backward(g.float())
+    assert _rel(W.grad, Wr.grad) < 1e-2
+    assert _rel(P.grad, Pr.grad) < 1e-2
+    # vocab shard: ids outside [500, 1000) give zeros
+    Ws = W.detach()[500:].contiguous()
+    out2 = ops.embedding(ids, Ws, vocab_start=500)
+    ref2 = torch.where((ids >= 500)[..., None], W.detach().float()[ids], torch.zeros(()))
+    assert _rel(out2, ref2) < 1e-2
+
+
+# ---------------------------------------------------------------- attention
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_flash_attention(D, causal, p):
+    from fleetx_amd import ops
+    B, S, H = 2, 384, 4
+    qkv = (0.5 * torch.randn(B, S, H, 3, D, device=DEV)).bfloat16().requires_grad_()
+    key = 123456789
+    out = ops.flash_attention_qkvpacked(qkv, causal=causal, dropout_p=p, key=key)
+    ref_in = qkv.detach().float().requires_grad_()
+    ref = ops.attention_reference(ref_in[:, :, :, 0], ref_in[:, :, :, 1], ref_in[:, :, :, 2],
+                                  causal=causal, dropout_p=p, key=key)
+    assert _rel(out, ref) < 2e-2, _rel(out, ref)
+    g = torch.randn_like(ref)
+    out.backward(g.bfloat16())
+    ref.backward(g)
+    for i in range(3):
+        assert _rel(qkv.grad[:, :, :, i], ref_in.grad[:, :, :, i]) < 3e-2, (i, _rel(
+            qkv.grad[:, :, :, i], ref_in.grad[:, :, :, i]))
+
+
+def test_flash_attention_tail_and_kvlens():
+    from fleetx_amd import ops
+    B, S, H, D = 2, 200, 2, 128
+    q = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    lens = torch.tensor([150, 200], device=DEV, dtype=torch.int32)
+    out = ops.flash_attention(q, k, v, causal=False, kv_lens=lens)
+    qr, kr, vr = [t.detach().float().requires_grad_() for t in (q, k, v)]
+    ref = ops.attention_reference(qr, kr, vr, causal=False, kv_lens=lens)
+    assert _rel(out, ref) < 2e-2
+    g = torch.randn_like(ref)
+    out.backward(g.bfloat16())
+    ref.backward(g)
+    for a, r in ((q, qr), (k, kr), (v, vr)):
+        assert _rel(a.grad, r.grad) < 3e-2
+
+
+def test_decode_attention():
+    from fleetx_amd import ops
+    B, H, D, L = 3, 4, 128, 300
+    q = torch.randn(B, H, D, device=DEV, dtype=torch.bfloat16)
+    kc = torch.randn(B, L, H, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.randn(B, L, H, D, device=DEV, dtype=torch.bfloat16)
+    lens = torch.tensor([300, 17, 128], device=DEV, dtype=torch.int32)
+    out = ops.decode_attention(q, kc, vc, lens)
+    ref = ops.decode_attention(q.cpu().float(), kc.cpu().float(), vc.cpu().float(), lens.cpu())
+    assert _rel(out.cpu(), ref) < 1e-2
+
+
+# ---------------------------------------------------------------- optimizer
+def test_fused_adamw_matches_torch():
+    from fleetx_amd.parallel.grad_buffer import FlatParamGradBuffer
+    from fleetx_amd.optims.optimizer import FusedAdamW, ClipGradByGlobalNorm
+    torch.manual_seed(1)
+    lin = torch.nn.Linear(256, 512).cuda().bfloat16()
+    ref = torch.nn.Linear(256, 512).cuda()
+    with torch.no_grad():
+        ref.weight.copy_(lin.weight.float())
+        ref.bias.copy_(lin.bias.float())
+    buf = FlatParamGradBuffer(lin.named_parameters())
+    opt = FusedAdamW(1e-2, buf, grad_clip=ClipGradByGlobalNorm(0.5), weight_decay=0.1)
+    topt = torch.optim.AdamW([{"params": [ref.weight], "weight_decay": 0.1},
+                              {"params": [ref.bias], "weight_decay": 0.0}], lr=1e-2,
+                             eps=1e-8)
+    for _ in range(3):
+        x = torch.randn(64, 256, device=DEV)
+        lin(x.bfloat16()).float().pow(2).mean().backward()
+        buf.finish()
+        g = [p.main_grad.float().clone() for _, p in buf.params]
+        ref.weight.grad = dict((id(p), gg) for (_, p), gg in zip(buf.params, g))[id(lin.weight)].clone()
+        ref.bias.grad = dict((id(p), gg) for (_, p), gg in zip(buf.params, g))[id(lin.bias)].clone()
+        torch.nn.utils.clip_grad_norm_(ref.parameters(), 0.5)
+        opt.step()
+        opt.clear_grad()
+        topt.step()
+        topt.zero_grad()
+    assert _rel(lin.weight, ref.weight) < 1e-2
+    assert _rel(lin.bias, ref.bias) < 1e-2
+
+
+def test_fake_quant():
+    from fleetx_amd.ops import quant
+    x = torch.randn(1000, device=DEV, dtype=torch.bfloat16)
+    s = quant.absmax(x)
+    assert abs(s.item() - x.float().abs().max().item()) < 1e-6
+    y = quant.fake_quant(x, s, 8)
+    yr = quant.fake_quant(x.cpu().float(), s.cpu(), 8)
+    assert _rel(y.cpu(), yr) < 1e-2
+
+
+# ---------------------------------------------------------------- end-to-end
+def test_gpt_train_step_loss_decreases():
+    from fleetx_amd.models.language_model.gpt.model import (GPTConfig, GPTForPretraining,
+                                                            GPTPretrainingCriterion)
+    from fleetx_amd.parallel.grad_buffer import FlatParamGradBuffer
+    from fleetx_amd.optims.optimizer import FusedAdamW, ClipGradByGlobalNorm
+    cfg = GPTConfig(vocab_size=2048, hidden_size=256, num_layers=2, num_attention_heads=4,
+                    max_position_embeddings=256, dtype=torch.bfloat16)
+    model = GPTForPretraining(cfg).cuda()
+    crit = GPTPretrainingCriterion(cfg)
+    buf = FlatParamGradBuffer(model.named_parameters())
+    opt = FusedAdamW(2e-3, buf, grad_clip=ClipGradByGlobalNorm(1.0))
+    toks = torch.randint(0, 2048, (4, 257), device=DEV)
+    losses = []
+    for _ in range(8):
+        loss = crit(model(toks[:, :-1]), toks[:, 1:], torch.ones(4, 256, device=DEV))
+        loss.backward()
+        buf.finish()
+        opt.step()
+        opt.clear_grad()
+        losses.append(loss.item())
+    assert abs(losses[0] - math.log(2048)) < 0.5
+    assert losses[-1] < losses[0] - 0.5, losses
