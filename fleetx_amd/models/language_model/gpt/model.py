@@ -188,12 +188,16 @@ class GPTDecoderLayer(nn.Module):
     def _attn_block(self, x):
         return self.attn(self.ln1(x))
 
+    def _attn_block_out(self, x):
+        return self._attn_block(x)[0]
+
     def _forward(self, x):
         cfg = self.cfg
         p = cfg.hidden_dropout_prob if self.training else 0.0
         stream = "local_seed" if cfg.sequence_parallel else "global_seed"
         if cfg.recompute_granularity == "full_attn" and self.training:
-            a, ab = recompute(self._attn_block, x)
+            # the out-proj bias is a leaf: pass it around the checkpoint, not through it
+            a, ab = recompute(self._attn_block_out, x), self.attn.out_proj.bias
         else:
             a, ab = self._attn_block(x)
         k1 = _key(stream) if p > 0 else 0

@@ -74,6 +74,13 @@ class Bucket:
         self.launched = False
 
 
+def _is_gloo(g):
+    try:
+        return dist.get_backend(g.group) == "gloo"
+    except Exception:
+        return False
+
+
 def default_decay_fn(name, p):
     """Reference rule: no decay for biases and norm params (``optimizer.py:39-43``)."""
     if p.ndim < 2:
@@ -86,7 +93,7 @@ class FlatParamGradBuffer:
 
     def __init__(self, named_params, dp_group=None, shard_group=None, mp_group=None,
                  embed_group=None, bucket_mb=256, overlap=True, shard_stage=0,
-                 decay_fn=default_decay_fn, reduce_dtype=torch.float32):
+                 decay_fn=default_decay_fn, reduce_dtype=torch.float32, fused_wgrad=True):
         named = [(n, p) for n, p in named_params if p.requires_grad]
         assert named, "no trainable parameters"
         self.dtype = named[0][1].dtype
@@ -101,7 +108,7 @@ class FlatParamGradBuffer:
 
         cats = {}
         for n, p in reversed(named):
-            key = (bool(decay_fn(n, p)), bool(getattr(p, "is_distributed", False)),
+            key = (bool(decay_fn(n, p)), bool(getattr(p, "tp_split", False)),
                    bool(getattr(p, "sequence_parallel", False)),
                    bool(getattr(p, "norm_exclude", False)))
             cats.setdefault(key, Category(key)).params.append((n, p))
@@ -132,6 +139,8 @@ class FlatParamGradBuffer:
                 p.data = view
                 p.main_grad = self.grad_flat[o:o + k].view_as(p)
                 p.grad = None
+                p._fx_fresh = True
+                p._fx_fused_wgrad = bool(getattr(p, "_fx_fused_wgrad_ok", False)) and fused_wgrad
                 self.params.append((n, p))
 
         # buckets: contiguous slices inside a category, capped at bucket_mb
@@ -171,17 +180,30 @@ class FlatParamGradBuffer:
     def _install_hooks(self):
         for n, p in self.params:
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(p)))
+            p._fx_grad_ready = self._make_ready(p)
+
+    def _make_ready(self, p):
+        def ready():
+            b = self._bucket_of[id(p)]
+            b.ready += 1
+            if b.ready == len(b.params) and self._last_micro and self.overlap:
+                self._launch(b)
+        return ready
 
     def _make_hook(self, p):
         def hook(param):
             g = param.grad
-            if g is not None:
+            if g is None:
+                # fires with no grad when a fused-wgrad Function already wrote
+                # main_grad and returned None: readiness was signalled there
+                return
+            if param._fx_fresh:
+                param.main_grad.copy_(g)
+            else:
                 param.main_grad.add_(g)
-                param.grad = None
-            b = self._bucket_of[id(param)]
-            b.ready += 1
-            if b.ready == len(b.params) and self._last_micro and self.overlap:
-                self._launch(b)
+            param._fx_fresh = False
+            param.grad = None
+            param._fx_grad_ready()
         return hook
 
     # ------------------------------------------------------------------ control
@@ -192,7 +214,9 @@ class FlatParamGradBuffer:
             b.ready = 0
 
     def zero_grad(self):
-        self.grad_flat.zero_()
+        # no fill: the first gradient write of a step overwrites (beta = 0)
+        for n, p in self.params:
+            p._fx_fresh = True
         for b in self.buckets:
             b.ready = 0
             b.work = None
@@ -208,13 +232,17 @@ class FlatParamGradBuffer:
         seg = self.grad_flat[b.start:b.end]
         works = []
         if self.shard_stage >= 1 and self.shard_group is not None:
-            # reduce-scatter to the owner; dp all-reduce of the owned shard
+            # reduce-scatter to the owner (in place: RCCL's recvbuff = sendbuff + rank*count);
+            # dp all-reduce of the owned shard follows in finish()
             n = self.shard_group.nranks
             r = self.shard_group.rank
             chunk = (b.end - b.start) // n
             out = self.grad_flat[b.start + r * chunk:b.start + (r + 1) * chunk]
-            works.append(dist.reduce_scatter_tensor(out, seg, group=self.shard_group.group,
-                                                    async_op=True))
+            if _is_gloo(self.shard_group):
+                works.append(dist.all_reduce(seg, group=self.shard_group.group, async_op=True))
+            else:
+                works.append(dist.reduce_scatter_tensor(out, seg, group=self.shard_group.group,
+                                                        async_op=True))
             b.work = ("rs", works, out)
         else:
             grp = self.dp_group
@@ -224,6 +252,10 @@ class FlatParamGradBuffer:
 
     def finish(self):
         """Complete every gradient collective; average over the data world."""
+        for n, p in self.params:
+            if p._fx_fresh:  # no gradient this step
+                p.main_grad.zero_()
+                p._fx_fresh = False
         for b in self.buckets:
             if not b.launched:
                 self._launch(b)
@@ -275,11 +307,17 @@ class FlatParamGradBuffer:
             return
         n = self.shard_group.nranks
         r = self.shard_group.rank
+        gloo = _is_gloo(self.shard_group)
         for b in self.buckets:
             chunk = (b.end - b.start) // n
             full = self.param_flat[b.start:b.end]
             mine = full[r * chunk:(r + 1) * chunk].clone()
-            dist.all_gather_into_tensor(full, mine, group=self.shard_group.group)
+            if gloo:
+                parts = list(full.view(n, chunk).unbind(0))
+                dist.all_gather(parts, mine, group=self.shard_group.group)
+                full.copy_(torch.cat(parts))
+            else:
+                dist.all_gather_into_tensor(full, mine, group=self.shard_group.group)
 
     def remove_hooks(self):
         for h in self._hooks:

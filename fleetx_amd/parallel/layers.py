@@ -28,6 +28,7 @@ import torch.nn.functional as F
 from . import mappings as M
 from . import topology as topo
 from .. import ops
+from .linear import linear
 
 
 def _param_seed(base_seed, name):
@@ -89,12 +90,13 @@ class ColumnParallelLinear(nn.Module):
         self.weight = nn.Parameter(init_full_then_slice((out_features, in_features), std,
                                                         name + ".weight", dim=0, dtype=dtype,
                                                         device=device))
-        self.weight.is_distributed = t > 1
+        self.weight.tp_split = t > 1
+        self.weight._fx_fused_wgrad_ok = True
         if bias:
             self.bias = nn.Parameter(init_full_then_slice((out_features,), 0.0, name + ".bias",
                                                           dim=0, dtype=dtype, device=device,
                                                           init="zeros"))
-            self.bias.is_distributed = t > 1
+            self.bias.tp_split = t > 1
         else:
             self.register_parameter("bias", None)
 
@@ -104,9 +106,9 @@ class ColumnParallelLinear(nn.Module):
         else:
             x = M.copy_to_mp(x)
         if self.skip_bias_add:
-            y = F.linear(x, self.weight)
+            y = linear(x, self.weight)
         else:
-            y = F.linear(x, self.weight, self.bias)
+            y = linear(x, self.weight, self.bias)
         if self.gather_output:
             y = M.gather_from_mp(y)
         if self.skip_bias_add:
@@ -130,7 +132,8 @@ class RowParallelLinear(nn.Module):
         self.weight = nn.Parameter(init_full_then_slice((out_features, in_features), std,
                                                         name + ".weight", dim=1, dtype=dtype,
                                                         device=device))
-        self.weight.is_distributed = t > 1
+        self.weight.tp_split = t > 1
+        self.weight._fx_fused_wgrad_ok = True
         if bias:
             self.bias = nn.Parameter(init_full_then_slice((out_features,), 0.0, name + ".bias",
                                                           dtype=dtype, device=device,
@@ -142,7 +145,7 @@ class RowParallelLinear(nn.Module):
     def forward(self, x):
         if not self.input_is_parallel:
             x = M.scatter_to_mp(x)
-        y = F.linear(x, self.weight)
+        y = linear(x, self.weight)
         if self.sequence_parallel:
             y = M.reduce_scatter_seq(y)
         else:
@@ -165,7 +168,7 @@ class VocabParallelEmbedding(nn.Module):
         self.vocab_start = r * self.per_rank
         self.weight = nn.Parameter(init_full_then_slice((vocab_size, hidden), std, name + ".weight",
                                                         dim=0, dtype=dtype, device=device))
-        self.weight.is_distributed = t > 1
+        self.weight.tp_split = t > 1
 
     def forward(self, ids, pos_ids=None, pos_weight=None, reduce=True):
         out = ops.embedding(ids, self.weight, pos_ids, pos_weight, self.vocab_start)

@@ -31,6 +31,16 @@ class P2P:
         self.ranks = g.ranks if g is not None else [0]
         self.stage = hcg.pp_rank
         self.nstages = hcg.pp_degree
+        self._warm = False
+
+    def warmup(self, device):
+        """One collective over the pipe group before the first grouped p2p
+        call: RCCL/NCCL require every rank of the group to take part in the
+        call that creates the communicator."""
+        if not self._warm and self.group is not None and self.nstages > 1:
+            t = torch.zeros(1, device=device)
+            dist.all_reduce(t, group=self.group)
+        self._warm = True
 
     def _peer(self, delta):
         return self.ranks[(self.stage + delta) % self.nstages]
@@ -71,6 +81,7 @@ class PipelineSchedule:
         self.act_shape_fn = act_shape_fn
         self.dtype, self.device = dtype, device
         self.num_chunks = num_chunks
+        self.p2p.warmup(device)
 
     def _buf(self):
         return torch.empty(self.act_shape_fn(), dtype=self.dtype, device=self.device)

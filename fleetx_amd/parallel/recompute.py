@@ -33,6 +33,10 @@ class _Recompute(torch.autograd.Function):
         ctx.save_for_backward(*tensors)
         with torch.no_grad():
             out = fn(*args)
+        for o in (out if isinstance(out, tuple) else (out,)):
+            if isinstance(o, torch.nn.Parameter):
+                raise ValueError("recompute segments must not return parameters; "
+                                 "return them outside the checkpointed function")
         ctx.rng_after = tracker.get_states()
         ctx.tuple_out = isinstance(out, tuple)
         return out
