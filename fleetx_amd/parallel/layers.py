@@ -28,7 +28,11 @@ import torch.nn.functional as F
 from . import mappings as M
 from . import topology as topo
 from .. import ops
-from .linear import linear
+from .linear import linear, column_tp_linear, row_tp_linear
+
+
+# Tensor-parallel comm/compute overlap switches (Distributed.comm.tp_overlap*)
+TP_OVERLAP = {"enabled": True, "row_chunks": 2}
 
 
 def _param_seed(base_seed, name):
@@ -101,14 +105,15 @@ class ColumnParallelLinear(nn.Module):
             self.register_parameter("bias", None)
 
     def forward(self, x):
+        b = None if self.skip_bias_add else self.bias
         if self.sequence_parallel:
             x = M.all_gather_seq(x)
+            y = linear(x, self.weight, b)
+        elif topo.mp_world_size() > 1 and TP_OVERLAP["enabled"]:
+            y = column_tp_linear(x, self.weight, b, topo.mp_group())
         else:
             x = M.copy_to_mp(x)
-        if self.skip_bias_add:
-            y = linear(x, self.weight)
-        else:
-            y = linear(x, self.weight, self.bias)
+            y = linear(x, self.weight, b)
         if self.gather_output:
             y = M.gather_from_mp(y)
         if self.skip_bias_add:
@@ -145,11 +150,12 @@ class RowParallelLinear(nn.Module):
     def forward(self, x):
         if not self.input_is_parallel:
             x = M.scatter_to_mp(x)
-        y = linear(x, self.weight)
         if self.sequence_parallel:
-            y = M.reduce_scatter_seq(y)
+            y = M.reduce_scatter_seq(linear(x, self.weight))
+        elif topo.mp_world_size() > 1 and TP_OVERLAP["enabled"]:
+            y = row_tp_linear(x, self.weight, topo.mp_group(), TP_OVERLAP["row_chunks"])
         else:
-            y = M.reduce_from_mp(y)
+            y = M.reduce_from_mp(linear(x, self.weight))
         if self.skip_bias_add:
             return y, self.bias
         return y + self.bias if self.bias is not None else y
