@@ -1,0 +1,1 @@
+from .gpt_tokenizer import GPTTokenizer, bytes_to_unicode  # noqa: F401
