@@ -88,6 +88,13 @@ def _split_micro(batch, n):
     return [batch] * n
 
 
+def _safe_len(loader):
+    try:
+        return len(loader)
+    except TypeError:
+        return -1
+
+
 class EagerEngine(BasicEngine):
     def __init__(self, configs, module, optimizer=None, lr=None, mode="train"):
         super().__init__()
@@ -223,6 +230,9 @@ class EagerEngine(BasicEngine):
             global_step, done = self._train_one_epoch(ep, train_data_loader, valid_data_loader,
                                                       global_step)
             self._module.training_epoch_end({"epoch": ep, "train_cost": time.time() - t_epoch})
+            if self._run_mode == "epoch" and valid_data_loader is not None and \
+                    (ep + 1) % self._eval_freq == 0:
+                self._evaluate_impl(ep, valid_data_loader, None)
             if self._run_mode == "epoch" and (ep + 1) % self._save_epoch == 0:
                 self.save(epoch=ep + 1, step=global_step)
             if done:
@@ -233,6 +243,7 @@ class EagerEngine(BasicEngine):
 
     def _train_one_epoch(self, epoch, loader, valid_loader, global_step):
         gbs = self._configs.Global.global_batch_size
+        total = _safe_len(loader)
         loss_acc, n_acc = None, 0
         t0 = time.time()
         for batch in loader:
@@ -255,7 +266,8 @@ class EagerEngine(BasicEngine):
                         raise FloatingPointError(msg)
                     logger.warning(msg)
                 self._module.training_step_end({"epoch": epoch, "batch": global_step, "loss": lval,
-                                                "train_cost": cost, "lr": self._current_lr()})
+                                                "train_cost": cost, "lr": self._current_lr(),
+                                                "total_batch": total})
                 loss_acc, n_acc = None, 0
                 t0 = time.time()
             if self._run_mode == "step" and valid_loader is not None and \
@@ -290,9 +302,10 @@ class EagerEngine(BasicEngine):
         model = self._module.model
         model.eval()
         outs = []
-        t0 = time.time()
+        total = _safe_len(loader)
+        t0 = t_start = time.time()
         for i, batch in enumerate(loader):
-            if i >= iters:
+            if iters is not None and i >= iters:
                 break
             batch = _to_device(batch, self.device)
             if self._pipeline:
@@ -306,8 +319,10 @@ class EagerEngine(BasicEngine):
             if (i + 1) % self._logging_freq == 0:
                 lval = float(loss.float().item()) if torch.is_tensor(loss) else loss
                 self._module.validation_step_end({"epoch": epoch, "batch": i, "loss": lval,
-                                                  "eval_cost": cost / self._logging_freq})
+                                                  "eval_cost": cost / self._logging_freq,
+                                                  "total_batch": total})
                 t0 = time.time()
+        self._module.validation_epoch_end({"epoch": epoch, "eval_cost": time.time() - t_start})
         model.train()
         return outs
 
@@ -315,16 +330,18 @@ class EagerEngine(BasicEngine):
         model = self._module.model
         model.eval()
         outs = []
-        t0 = time.time()
+        total = _safe_len(valid_data_loader)
+        t0 = t_start = time.time()
         with torch.no_grad():
             for i, batch in enumerate(valid_data_loader):
                 batch = _to_device(batch, self.device)
                 out = self._module.validation_step(batch)
                 self._module.validation_step_end({"epoch": epoch, "batch": i, "loss": out,
-                                                  "eval_cost": time.time() - t0})
+                                                  "eval_cost": time.time() - t0,
+                                                  "total_batch": total})
                 outs.append(out)
                 t0 = time.time()
-        self._module.validation_epoch_end({"epoch": epoch})
+        self._module.validation_epoch_end({"epoch": epoch, "eval_cost": time.time() - t_start})
         return outs
 
     @torch.no_grad()

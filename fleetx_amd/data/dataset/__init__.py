@@ -13,3 +13,12 @@ DATASETS = {
 def register_dataset(name, cls):
     DATASETS[name] = cls
     return cls
+
+
+def _register_optional():
+    from .vision_dataset import GeneralClsDataset, ImageFolder, CIFAR, SyntheticImageDataset
+    for c in (GeneralClsDataset, ImageFolder, CIFAR, SyntheticImageDataset):
+        DATASETS[c.__name__] = c
+
+
+_register_optional()

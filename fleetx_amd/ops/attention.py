@@ -119,11 +119,28 @@ class _PackedEntry(torch.autograd.Function):
         return grads[3], None, None, None, None, None
 
 
+def _padded_dim(d):
+    return 64 if d <= 64 else 128
+
+
 def flash_attention(q, k, v, causal=True, dropout_p=0.0, key=0, scale=None, kv_lens=None):
-    """q: [B, Sq, H, D], k/v: [B, Sk, H, D] (strided views allowed)."""
-    scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    """q: [B, Sq, H, D], k/v: [B, Sk, H, D] (strided views allowed).
+
+    Head dims other than 64/128 (e.g. ViT-g's 88) are zero-padded to the next
+    kernel tile width: zero columns add nothing to QK^T and produce zero output
+    columns that are sliced off (the softmax scale keeps the true ``D``)."""
+    D = q.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if not q.is_cuda:
         return attention_reference(q, k, v, causal, dropout_p, key, scale, kv_lens)
+    if D not in (64, 128):
+        if D > 128:
+            raise NotImplementedError("head_dim > 128 is not supported by the flash kernel")
+        P = _padded_dim(D) - D
+        pad = lambda t: torch.nn.functional.pad(t, (0, P))  # noqa: E731
+        out = _FlashAttn.apply(pad(q), pad(k), pad(v), None, causal, float(dropout_p), key,
+                               scale, kv_lens)
+        return out[..., :D]
     return _FlashAttn.apply(q, k, v, None, causal, float(dropout_p), key, scale, kv_lens)
 
 

@@ -267,3 +267,44 @@ def test_gpt_train_step_loss_decreases():
         losses.append(loss.item())
     assert abs(losses[0] - math.log(2048)) < 0.5
     assert losses[-1] < losses[0] - 0.5, losses
+
+
+@pytest.mark.parametrize("D", [40, 88])
+def test_flash_attention_padded_head_dim(D):
+    """Head dims outside {64,128} (ViT-g: 88) go through zero-padded tiles."""
+    from fleetx_amd import ops
+    B, S, H = 2, 257, 4  # ViT-style odd token count (cls + 16x16 patches)
+    q, k, v = [torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+               for _ in range(3)]
+    out = ops.flash_attention(q, k, v, causal=False)
+    assert out.shape == (B, S, H, D)
+    qr, kr, vr = [t.detach().float().requires_grad_() for t in (q, k, v)]
+    ref = ops.attention_reference(qr, kr, vr, causal=False)
+    assert _rel(out, ref) < 2e-2
+    g = torch.randn_like(ref)
+    out.backward(g.bfloat16())
+    ref.backward(g)
+    for a, r in ((q, qr), (k, kr), (v, vr)):
+        assert _rel(a.grad, r.grad) < 3e-2
+
+
+def test_vit_train_step_on_gpu():
+    from fleetx_amd.models.vision_model.vit import ViT
+    from fleetx_amd.models.vision_model.loss import ViTCELoss
+    from fleetx_amd.parallel.grad_buffer import FlatParamGradBuffer
+    from fleetx_amd.optims.optimizer import FusedAdamW
+    m = ViT(img_size=64, patch_size=8, class_num=10, embed_dim=256, depth=2, num_heads=4,
+            qkv_bias=True, epsilon=1e-6).cuda().bfloat16()
+    buf = FlatParamGradBuffer(m.named_parameters())
+    opt = FusedAdamW(1e-3, buf)
+    x = torch.randn(8, 3, 64, 64, device=DEV)
+    y = torch.arange(8, device=DEV) % 10
+    losses = []
+    for _ in range(10):
+        loss = ViTCELoss()(m(x), y)
+        loss.backward()
+        buf.finish()
+        opt.step()
+        opt.clear_grad()
+        losses.append(loss.item())
+    assert losses[-1] < losses[0], losses
