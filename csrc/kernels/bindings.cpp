@@ -42,12 +42,12 @@ void fx_embedding_fwd(int, const int64_t*, const int64_t*, const void*, const vo
 void fx_embedding_bwd(int, const int64_t*, const void*, float*, int, int, long, long,
                       hipStream_t);
 int fx_flash_fwd(const void*, const void*, const void*, void*, float*, const long*, const long*,
-                 const long*, const long*, const int*, int, int, int, int, int, int, float, float,
-                 uint64_t, hipStream_t);
+                 const long*, const long*, const int*, const float*, long, int, int, int, int, int,
+                 int, float, float, uint64_t, hipStream_t);
 int fx_flash_bwd(const void*, const void*, const void*, const void*, const void*, const float*,
                  float*, void*, void*, void*, const long*, const long*, const long*, const long*,
-                 const long*, const long*, const int*, int, int, int, int, int, int, float, float,
-                 uint64_t, hipStream_t);
+                 const long*, const long*, const int*, const float*, long, int, int, int, int, int,
+                 int, float, float, uint64_t, hipStream_t);
 int fx_fake_quant_fwd(int, const void*, void*, const float*, int, long, hipStream_t);
 void fx_absmax(int, const void*, long, float*, hipStream_t);
 int fx_decode_attn(const void*, const void*, const void*, void*, const int*, int, int, int, int,
@@ -145,23 +145,23 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.def("flash_fwd", [](ptr q, ptr k, ptr v, ptr out, ptr lse, std::vector<long> qs,
                         std::vector<long> ks, std::vector<long> vs, std::vector<long> os,
-                        ptr kv_lens, int B, int H, int Sq, int Sk, int D, int causal, float scale,
-                        float p, uint64_t key, ptr st) {
+                        ptr kv_lens, ptr kbias, long kb_stride, int B, int H, int Sq, int Sk, int D,
+                        int causal, float scale, float p, uint64_t key, ptr st) {
     auto a = v3(qs), b = v3(ks), c = v3(vs), d = v3(os);
     return fx_flash_fwd(CP(q), CP(k), CP(v), P(out), F(lse), a.data(), b.data(), c.data(),
-                        d.data(), reinterpret_cast<const int*>(kv_lens), B, H, Sq, Sk, D, causal,
-                        scale, p, key, S(st));
+                        d.data(), reinterpret_cast<const int*>(kv_lens), F(kbias), kb_stride, B, H,
+                        Sq, Sk, D, causal, scale, p, key, S(st));
   });
   m.def("flash_bwd", [](ptr q, ptr k, ptr v, ptr o, ptr dout, ptr lse, ptr delta, ptr dq, ptr dk,
                         ptr dv, std::vector<long> qs, std::vector<long> ks, std::vector<long> vs,
                         std::vector<long> os, std::vector<long> dqs, std::vector<long> dks,
-                        ptr kv_lens, int B, int H, int Sq, int Sk, int D, int causal, float scale,
-                        float p, uint64_t key, ptr st) {
+                        ptr kv_lens, ptr kbias, long kb_stride, int B, int H, int Sq, int Sk, int D,
+                        int causal, float scale, float p, uint64_t key, ptr st) {
     auto a = v3(qs), b = v3(ks), c = v3(vs), d = v3(os), e = v3(dks), f = v3(dqs);
     return fx_flash_bwd(CP(q), CP(k), CP(v), CP(o), CP(dout), F(lse), F(delta), P(dq), P(dk),
                         P(dv), a.data(), b.data(), c.data(), d.data(), f.data(), e.data(),
-                        reinterpret_cast<const int*>(kv_lens), B, H, Sq, Sk, D, causal, scale, p,
-                        key, S(st));
+                        reinterpret_cast<const int*>(kv_lens), F(kbias), kb_stride, B, H, Sq, Sk,
+                        D, causal, scale, p, key, S(st));
   });
   m.def("fake_quant_fwd", [](int dt, ptr x, ptr y, ptr scale, int bits, long n, ptr st) {
     return fx_fake_quant_fwd(dt, CP(x), P(y), F(scale), bits, n, S(st));

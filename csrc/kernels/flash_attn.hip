@@ -107,6 +107,8 @@ struct AttnParams {
   uint16_t *out, *dq, *dk, *dv;
   float *lse, *delta;
   const int* kv_lens;
+  const float* kbias;      // optional additive key bias [B, kb_b] (natural-log units)
+  long kb_b;
   long sq_b, sq_s, sq_h;   // q strides (elements) batch / seq / head
   long sk_b, sk_s, sk_h;   // k (and v) strides
   long sv_b, sv_s, sv_h;
@@ -119,6 +121,24 @@ struct AttnParams {
   float drop_scale;
 };
 
+// S^T tile rows are keys: register i of lane half h holds key crow(i, h) of
+// its 32-row block.  Keys crow(4g..4g+3, h) = 8g + 4h + {0..3} are contiguous,
+// so the bias arrives as one float4 per group.  Result: s*scale*log2e + bias*log2e.
+__device__ __forceinline__ void key_bias_add1(floatx16& acc, const float* kb, int h, float sl2) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float4 v = *reinterpret_cast<const float4*>(kb + 8 * g + 4 * h);
+    acc[4 * g + 0] = acc[4 * g + 0] * sl2 + v.x * LOG2E;
+    acc[4 * g + 1] = acc[4 * g + 1] * sl2 + v.y * LOG2E;
+    acc[4 * g + 2] = acc[4 * g + 2] * sl2 + v.z * LOG2E;
+    acc[4 * g + 3] = acc[4 * g + 3] * sl2 + v.w * LOG2E;
+  }
+}
+__device__ __forceinline__ void key_bias_add(floatx16 (&acc)[2], const float* kb, int h, float sl2) {
+  key_bias_add1(acc[0], kb, h, sl2);
+  key_bias_add1(acc[1], kb + 32, h, sl2);
+}
+
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
   const int xcd = bid & 7, pos = bid >> 3, q = nblk >> 3, r = nblk & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
@@ -127,7 +147,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
 // ============================================================================
 // forward: WG = 4 waves x 32 queries = 128 queries; KV tile = 64 keys
 // ============================================================================
-template <int D, bool CAUSAL, bool DROP>
+template <int D, bool CAUSAL, bool DROP, bool KB>
 __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KV = 64, TB = KV * D * 2;
@@ -199,11 +219,12 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
       }
       const bool need_mask = (CAUSAL && kb + KV - 1 > wq0) || (kb + KV > kv_len);
       float mloc = -INFINITY;
+      if constexpr (KB) key_bias_add(sacc, P.kbias + (long)b * P.kb_b + kb, h, sl2);
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float x = sacc[t][i] * sl2;
+          float x = KB ? sacc[t][i] : sacc[t][i] * sl2;
           if (need_mask) {
             const int key = kb + 32 * t + crow(i, h);
             if ((CAUSAL && key > qi) || key >= kv_len) x = -INFINITY;
@@ -303,7 +324,7 @@ __global__ __launch_bounds__(256) void fa_bwd_pre_kernel(AttnParams P) {
 // backward dQ: WG = 4 waves x 32 queries; loop over 64-key tiles.
 //   S^T = K.Q^T, dP^T = V.dO^T (queries on lanes), dQ^T += K^T.dS^T
 // ============================================================================
-template <int D, bool CAUSAL, bool DROP>
+template <int D, bool CAUSAL, bool DROP, bool KB>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KV = 64, TB = KV * D * 2;
@@ -380,10 +401,12 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
           sacc = mfma(row_frag<D>(kt, 32 * t + (lane & 31), s, h), qf[s], sacc);
           dpacc = mfma(row_frag<D>(vt, 32 * t + (lane & 31), s, h), gf[s], dpacc);
         }
+        if constexpr (KB) key_bias_add1(sacc, P.kbias + (long)b * P.kb_b + kb + 32 * t, h, sl2);
 #pragma unroll
         for (int i = 0; i < 16; i += 2) {
           const int key = kb + 32 * t + crow(i, h);
-          float p0 = exp2f(sacc[i] * sl2 - lse2), p1 = exp2f(sacc[i + 1] * sl2 - lse2);
+          const float sc = KB ? 1.f : sl2;
+          float p0 = exp2f(sacc[i] * sc - lse2), p1 = exp2f(sacc[i + 1] * sc - lse2);
           if (need_mask) {
             if ((CAUSAL && key > qi) || key >= kv_len) p0 = 0.f;
             if ((CAUSAL && key + 1 > qi) || key + 1 >= kv_len) p1 = 0.f;
@@ -433,7 +456,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
 //   S = Q.K^T, dP = dO.V^T (keys on lanes, queries in registers)
 //   dV^T += dO^T.(P o Z),  dK^T += Q^T.dS
 // ============================================================================
-template <int D, bool CAUSAL, bool DROP>
+template <int D, bool CAUSAL, bool DROP, bool KB>
 __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int QT = 64, TB = QT * D * 2;
@@ -459,6 +482,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnParams P) {
   const int wk0 = kblock * 128 + w * 32;
   const int ki = wk0 + (lane & 31);
   const bool kvalid = ki < kv_len;
+  const float kb2 = KB ? P.kbias[(long)b * P.kb_b + ki] * LOG2E : 0.f;
   bf16x8 kf[D / 16], vf[D / 16];
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) {
@@ -508,7 +532,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnParams P) {
       for (int i = 0; i < 16; ++i) {
         const int ql_ = 32 * t + crow(i, h);
         const int q = qb + ql_;
-        float p = exp2f(sacc[i] * sl2 - lse_s[ql_]);
+        float p = exp2f(sacc[i] * sl2 + kb2 - lse_s[ql_]);
         if ((CAUSAL && ki > q) || !kvalid || q >= P.Sq) p = 0.f;
         float z = 1.f;
         if (DROP) {
@@ -577,47 +601,50 @@ AttnParams make_params(const void* q, const void* k, const void* v, const long* 
   return P;
 }
 
-template <template <int, bool, bool> class K>
-struct Dummy {};
-
 }  // namespace
 
-#define FA_DISPATCH(KERNEL, D, causal, drop, grid, smem, st, P)                         \
+#define FA_DISPATCH_D(KERNEL, DD, causal, drop, kbias, grid, smem, st, P)         \
+  do {                                                                          \
+    if (causal) {                                                               \
+      if (drop) KERNEL<DD, true, true, false><<<grid, 256, smem, st>>>(P);      \
+      else KERNEL<DD, true, false, false><<<grid, 256, smem, st>>>(P);          \
+    } else if (kbias) {                                                         \
+      if (drop) KERNEL<DD, false, true, true><<<grid, 256, smem, st>>>(P);      \
+      else KERNEL<DD, false, false, true><<<grid, 256, smem, st>>>(P);          \
+    } else {                                                                    \
+      if (drop) KERNEL<DD, false, true, false><<<grid, 256, smem, st>>>(P);     \
+      else KERNEL<DD, false, false, false><<<grid, 256, smem, st>>>(P);         \
+    }                                                                           \
+  } while (0)
+// key bias is only instantiated for non-causal attention (BERT-style padding
+// masks); causal + bias is rejected by the launchers.
+#define FA_DISPATCH(KERNEL, D, causal, drop, kbias, grid, smem, st, P)                  \
   do {                                                                                  \
-    if (D == 128) {                                                                     \
-      if (causal) {                                                                     \
-        if (drop) KERNEL<128, true, true><<<grid, 256, smem, st>>>(P);                  \
-        else KERNEL<128, true, false><<<grid, 256, smem, st>>>(P);                      \
-      } else {                                                                          \
-        if (drop) KERNEL<128, false, true><<<grid, 256, smem, st>>>(P);                 \
-        else KERNEL<128, false, false><<<grid, 256, smem, st>>>(P);                     \
-      }                                                                                 \
-    } else {                                                                            \
-      if (causal) {                                                                     \
-        if (drop) KERNEL<64, true, true><<<grid, 256, smem, st>>>(P);                   \
-        else KERNEL<64, true, false><<<grid, 256, smem, st>>>(P);                       \
-      } else {                                                                          \
-        if (drop) KERNEL<64, false, true><<<grid, 256, smem, st>>>(P);                  \
-        else KERNEL<64, false, false><<<grid, 256, smem, st>>>(P);                      \
-      }                                                                                 \
-    }                                                                                   \
+    if (D == 128) FA_DISPATCH_D(KERNEL, 128, causal, drop, kbias, grid, smem, st, P);   \
+    else FA_DISPATCH_D(KERNEL, 64, causal, drop, kbias, grid, smem, st, P);             \
   } while (0)
 
 // strides arrays are {batch, seq, head} in elements; head dim contiguous.
+// kbias: optional [B, kb_stride] float additive key bias; kb_stride must be
+// >= round_up(Sk, 128) (tiles read whole 64-key groups).
 extern "C" int fx_flash_fwd(const void* q, const void* k, const void* v, void* out, float* lse,
                             const long* qs, const long* ks, const long* vs, const long* os,
-                            const int* kv_lens, int B, int H, int Sq, int Sk, int D, int causal,
-                            float scale, float p, uint64_t key, hipStream_t st) {
+                            const int* kv_lens, const float* kbias, long kb_stride, int B, int H,
+                            int Sq, int Sk, int D, int causal, float scale, float p, uint64_t key,
+                            hipStream_t st) {
   if (D != 64 && D != 128) return -1;
+  if (kbias && (causal || kb_stride < ((Sk + 127) / 128) * 128)) return -2;
   AttnParams P = make_params(q, k, v, qs, ks, vs, B, H, Sq, Sk, scale, p, key);
   P.out = (uint16_t*)out;
   P.lse = lse;
   P.kv_lens = kv_lens;
+  P.kbias = kbias;
+  P.kb_b = kb_stride;
   P.so_b = os[0]; P.so_s = os[1]; P.so_h = os[2];
   const int nq = (Sq + 127) / 128;
   const int grid = nq * B * H;
   const size_t smem = 4 * 64 * D * 2;
-  FA_DISPATCH(fa_fwd_kernel, D, causal, p > 0.f, grid, smem, st, P);
+  FA_DISPATCH(fa_fwd_kernel, D, causal, p > 0.f, kbias != nullptr, grid, smem, st, P);
   return 0;
 }
 
@@ -626,10 +653,11 @@ extern "C" int fx_flash_bwd(const void* q, const void* k, const void* v, const v
                             const void* dout, const float* lse, float* delta, void* dq, void* dk,
                             void* dv, const long* qs, const long* ks, const long* vs,
                             const long* os, const long* dqs, const long* dks, const int* kv_lens,
-                            int B, int H,
+                            const float* kbias, long kb_stride, int B, int H,
                             int Sq, int Sk, int D, int causal, float scale, float p, uint64_t key,
                             hipStream_t st) {
   if (D != 64 && D != 128) return -1;
+  if (kbias && (causal || kb_stride < ((Sk + 127) / 128) * 128)) return -2;
   AttnParams P = make_params(q, k, v, qs, ks, vs, B, H, Sq, Sk, scale, p, key);
   P.o = (const uint16_t*)o;
   P.dout = (const uint16_t*)dout;
@@ -639,6 +667,8 @@ extern "C" int fx_flash_bwd(const void* q, const void* k, const void* v, const v
   P.dk = (uint16_t*)dk;
   P.dv = (uint16_t*)dv;
   P.kv_lens = kv_lens;
+  P.kbias = kbias;
+  P.kb_b = kb_stride;
   P.so_b = os[0]; P.so_s = os[1]; P.so_h = os[2];
   P.sdk_b = dks[0]; P.sdk_s = dks[1]; P.sdk_h = dks[2];
   P.sdq_b = dqs[0]; P.sdq_s = dqs[1]; P.sdq_h = dqs[2];
@@ -652,12 +682,13 @@ extern "C" int fx_flash_bwd(const void* q, const void* k, const void* v, const v
   {
     const int nq = (Sq + 127) / 128;
     const size_t smem = 4 * 64 * D * 2;
-    FA_DISPATCH(fa_bwd_dq_kernel, D, causal, p > 0.f, nq * B * H, smem, st, P);
+    FA_DISPATCH(fa_bwd_dq_kernel, D, causal, p > 0.f, kbias != nullptr, nq * B * H, smem, st, P);
   }
   {
     const int nk = (Sk + 127) / 128;
     const size_t smem = 2 * 64 * D * 2 + 2 * 64 * 4;
-    FA_DISPATCH(fa_bwd_dkdv_kernel, D, causal, p > 0.f, nk * B * H, smem, st, P);
+    FA_DISPATCH(fa_bwd_dkdv_kernel, D, causal, p > 0.f, kbias != nullptr, nk * B * H, smem, st,
+                P);
   }
   return 0;
 }

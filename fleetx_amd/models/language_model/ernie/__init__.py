@@ -1,0 +1,2 @@
+from .model import (ErnieModel, ErnieForPretraining, ErniePretrainingCriterion,  # noqa: F401
+                    ErnieForMaskedLM, ErnieForMultipleChoice, mlm_mask)

@@ -24,8 +24,12 @@ def _strides(t):
     return [t.stride(0), t.stride(1), t.stride(2)]
 
 
-def attention_reference(q, k, v, causal=True, dropout_p=0.0, key=0, scale=None, kv_lens=None):
-    """PyTorch math for ``[B, S, H, D]`` inputs (CPU path and test oracle)."""
+def attention_reference(q, k, v, causal=True, dropout_p=0.0, key=0, scale=None, kv_lens=None,
+                        key_bias=None):
+    """PyTorch math for ``[B, S, H, D]`` inputs (CPU path and test oracle).
+
+    ``key_bias``: optional additive ``[B, Sk]`` score bias (e.g. ``-1e4`` on
+    padding keys, the BERT/ERNIE convention)."""
     B, Sq, H, D = q.shape
     Sk = k.shape[1]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
@@ -33,6 +37,8 @@ def attention_reference(q, k, v, causal=True, dropout_p=0.0, key=0, scale=None, 
     kf = k.float().permute(0, 2, 1, 3)
     vf = v.float().permute(0, 2, 1, 3)
     s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if key_bias is not None:
+        s = s + key_bias.float().view(B, 1, 1, Sk)
     mask = torch.zeros(Sq, Sk, dtype=torch.bool, device=q.device)
     if causal:
         mask = torch.triu(torch.ones(Sq, Sk, dtype=torch.bool, device=q.device), diagonal=1)
@@ -52,7 +58,7 @@ def attention_reference(q, k, v, causal=True, dropout_p=0.0, key=0, scale=None, 
 
 class _FlashAttn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, packed, causal, p, key, scale, kv_lens):
+    def forward(ctx, q, k, v, packed, causal, p, key, scale, kv_lens, key_bias=None):
         # packed: None or the [B,S,H,3,D] tensor q/k/v are views of
         B, Sq, H, D = q.shape
         Sk = k.shape[1]
@@ -65,8 +71,10 @@ class _FlashAttn(torch.autograd.Function):
         out = torch.empty(B, Sq, H, D, device=q.device, dtype=q.dtype)
         lse = torch.empty(B * H * Sq, device=q.device, dtype=torch.float32)
         kl = kv_lens.to(torch.int32).contiguous() if kv_lens is not None else None
+        kb = _padded_bias(key_bias, B, Sk, q.device)
         rc = k_.flash_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), lse.data_ptr(),
                           _strides(q), _strides(k), _strides(v), _strides(out), _lib.ptr(kl),
+                          _lib.ptr(kb), kb.shape[1] if kb is not None else 0,
                           B, H, Sq, Sk, D, int(causal), float(scale), float(p), key,
                           _lib.stream())
         if rc != 0:
@@ -74,12 +82,12 @@ class _FlashAttn(torch.autograd.Function):
         _lib.maybe_sync()
         ctx.causal, ctx.p, ctx.key, ctx.scale = causal, p, key, scale
         ctx.packed = packed is not None
-        ctx.save_for_backward(q, k, v, out, lse, kl)
+        ctx.save_for_backward(q, k, v, out, lse, kl, kb)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        q, k, v, out, lse, kl = ctx.saved_tensors
+        q, k, v, out, lse, kl, kb = ctx.saved_tensors
         B, Sq, H, D = q.shape
         Sk = k.shape[1]
         dout = dout.contiguous()
@@ -95,35 +103,50 @@ class _FlashAttn(torch.autograd.Function):
             q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), dout.data_ptr(),
             lse.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
             _strides(q), _strides(k), _strides(v), _strides(out), _strides(dq), _strides(dk),
-            _lib.ptr(kl), B, H, Sq, Sk, D, int(ctx.causal), float(ctx.scale), float(ctx.p),
+            _lib.ptr(kl), _lib.ptr(kb), kb.shape[1] if kb is not None else 0,
+            B, H, Sq, Sk, D, int(ctx.causal), float(ctx.scale), float(ctx.p),
             ctx.key, _lib.stream())
         if rc != 0:
             raise RuntimeError("flash_bwd failed (%d)" % rc)
         _lib.maybe_sync()
         if ctx.packed:
-            return None, None, None, dqkv, None, None, None, None, None
-        return dq, dk, dv, None, None, None, None, None, None
+            return None, None, None, dqkv, None, None, None, None, None, None
+        return dq, dk, dv, None, None, None, None, None, None, None
 
 
 class _PackedEntry(torch.autograd.Function):
     """Routes the packed-QKV gradient back to the packed tensor."""
 
     @staticmethod
-    def forward(ctx, qkv, causal, p, key, scale, kv_lens):
+    def forward(ctx, qkv, causal, p, key, scale, kv_lens, key_bias):
         q, k, v = qkv[:, :, :, 0], qkv[:, :, :, 1], qkv[:, :, :, 2]
-        return _FlashAttn.forward(ctx, q, k, v, qkv, causal, p, key, scale, kv_lens)
+        return _FlashAttn.forward(ctx, q, k, v, qkv, causal, p, key, scale, kv_lens, key_bias)
 
     @staticmethod
     def backward(ctx, dout):
         grads = _FlashAttn.backward(ctx, dout)
-        return grads[3], None, None, None, None, None
+        return grads[3], None, None, None, None, None, None
+
+
+_WARNED = {}
+
+
+def _padded_bias(key_bias, B, Sk, device):
+    """fp32 ``[B, round_up(Sk, 128)]`` copy: the kernels read whole key groups."""
+    if key_bias is None:
+        return None
+    width = (Sk + 127) // 128 * 128
+    kb = torch.zeros(B, width, device=device, dtype=torch.float32)
+    kb[:, :Sk] = key_bias.reshape(B, Sk)
+    return kb
 
 
 def _padded_dim(d):
     return 64 if d <= 64 else 128
 
 
-def flash_attention(q, k, v, causal=True, dropout_p=0.0, key=0, scale=None, kv_lens=None):
+def flash_attention(q, k, v, causal=True, dropout_p=0.0, key=0, scale=None, kv_lens=None,
+                    key_bias=None):
     """q: [B, Sq, H, D], k/v: [B, Sk, H, D] (strided views allowed).
 
     Head dims other than 64/128 (e.g. ViT-g's 88) are zero-padded to the next
@@ -131,26 +154,37 @@ def flash_attention(q, k, v, causal=True, dropout_p=0.0, key=0, scale=None, kv_l
     columns that are sliced off (the softmax scale keeps the true ``D``)."""
     D = q.shape[-1]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if key_bias is not None and causal:
+        raise ValueError("key_bias is supported for non-causal attention only")
     if not q.is_cuda:
-        return attention_reference(q, k, v, causal, dropout_p, key, scale, kv_lens)
+        return attention_reference(q, k, v, causal, dropout_p, key, scale, kv_lens, key_bias)
     if D not in (64, 128):
         if D > 128:
-            raise NotImplementedError("head_dim > 128 is not supported by the flash kernel")
+            # wider heads than one MFMA tile row: exact fp32 math path (S x S materialised)
+            if not _WARNED.get(D):
+                _WARNED[D] = True
+                import warnings
+                warnings.warn("head_dim %d > 128: attention falls back to unfused math" % D)
+            return attention_reference(q, k, v, causal, dropout_p, key, scale, kv_lens, key_bias)
         P = _padded_dim(D) - D
         pad = lambda t: torch.nn.functional.pad(t, (0, P))  # noqa: E731
         out = _FlashAttn.apply(pad(q), pad(k), pad(v), None, causal, float(dropout_p), key,
-                               scale, kv_lens)
+                               scale, kv_lens, key_bias)
         return out[..., :D]
-    return _FlashAttn.apply(q, k, v, None, causal, float(dropout_p), key, scale, kv_lens)
+    return _FlashAttn.apply(q, k, v, None, causal, float(dropout_p), key, scale, kv_lens, key_bias)
 
 
-def flash_attention_qkvpacked(qkv, causal=True, dropout_p=0.0, key=0, scale=None, kv_lens=None):
+def flash_attention_qkvpacked(qkv, causal=True, dropout_p=0.0, key=0, scale=None, kv_lens=None,
+                              key_bias=None):
     """qkv: [B, S, H, 3, D] -> out [B, S, H, D]; gradient lands in one packed buffer."""
-    scale = scale if scale is not None else 1.0 / math.sqrt(qkv.shape[-1])
-    if not qkv.is_cuda:
-        return attention_reference(qkv[:, :, :, 0], qkv[:, :, :, 1], qkv[:, :, :, 2], causal,
-                                   dropout_p, key, scale, kv_lens)
-    return _PackedEntry.apply(qkv, causal, float(dropout_p), key, scale, kv_lens)
+    D = qkv.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if not qkv.is_cuda or D not in (64, 128):
+        return flash_attention(qkv[:, :, :, 0], qkv[:, :, :, 1], qkv[:, :, :, 2], causal,
+                               dropout_p, key, scale, kv_lens, key_bias)
+    if key_bias is not None and causal:
+        raise ValueError("key_bias is supported for non-causal attention only")
+    return _PackedEntry.apply(qkv, causal, float(dropout_p), key, scale, kv_lens, key_bias)
 
 
 def decode_attention(q, k_cache, v_cache, lens, scale=None):
