@@ -50,6 +50,15 @@ int fx_flash_bwd(const void*, const void*, const void*, const void*, const void*
                  int, float, float, uint64_t, hipStream_t);
 int fx_fake_quant_fwd(int, const void*, void*, const float*, int, long, hipStream_t);
 void fx_absmax(int, const void*, long, float*, hipStream_t);
+int fx_gn_nseg(long, long);
+int fx_gn_fwd(int, const void*, const float*, const float*, const float*, const float*, void*,
+              double*, float*, float*, int, int, int, long, int, float, int, hipStream_t);
+int fx_gn_bwd_reduce(int, const void*, const void*, const float*, const float*, const float*,
+                     const float*, const float*, const float*, float*, int, int, int, long, int,
+                     int, hipStream_t);
+int fx_gn_bwd_apply(int, const void*, const void*, const float*, const float*, const float*,
+                    const float*, const float*, const float*, const float*, const float*, void*,
+                    int, int, int, long, int, int, hipStream_t);
 int fx_decode_attn(const void*, const void*, const void*, void*, const int*, int, int, int, int,
                    int, long, long, long, long, long, long, float, hipStream_t);
 }
@@ -162,6 +171,26 @@ PYBIND11_MODULE(_kernels, m) {
                         P(dv), a.data(), b.data(), c.data(), d.data(), f.data(), e.data(),
                         reinterpret_cast<const int*>(kv_lens), F(kbias), kb_stride, B, H, Sq, Sk,
                         D, causal, scale, p, key, S(st));
+  });
+  m.def("gn_nseg", [](long rows, long hw) { return fx_gn_nseg(rows, hw); });
+  m.def("gn_fwd", [](int dt, ptr x, ptr gamma, ptr beta, ptr scale, ptr shift, ptr y, ptr part,
+                     ptr mean, ptr rstd, int B, int C, int G, long hw, int nseg, float eps,
+                     int silu, ptr st) {
+    return fx_gn_fwd(dt, CP(x), F(gamma), F(beta), F(scale), F(shift), P(y),
+                     reinterpret_cast<double*>(part), F(mean), F(rstd), B, C, G, hw, nseg, eps,
+                     silu, S(st));
+  });
+  m.def("gn_bwd_reduce", [](int dt, ptr x, ptr dy, ptr mean, ptr rstd, ptr gamma, ptr beta,
+                            ptr scale, ptr shift, ptr part, int B, int C, int G, long hw, int nseg,
+                            int silu, ptr st) {
+    return fx_gn_bwd_reduce(dt, CP(x), CP(dy), F(mean), F(rstd), F(gamma), F(beta), F(scale),
+                            F(shift), F(part), B, C, G, hw, nseg, silu, S(st));
+  });
+  m.def("gn_bwd_apply", [](int dt, ptr x, ptr dy, ptr mean, ptr rstd, ptr gamma, ptr beta,
+                           ptr scale, ptr shift, ptr g1, ptr g2, ptr dx, int B, int C, int G,
+                           long hw, int nseg, int silu, ptr st) {
+    return fx_gn_bwd_apply(dt, CP(x), CP(dy), F(mean), F(rstd), F(gamma), F(beta), F(scale),
+                           F(shift), F(g1), F(g2), P(dx), B, C, G, hw, nseg, silu, S(st));
   });
   m.def("fake_quant_fwd", [](int dt, ptr x, ptr y, ptr scale, int bits, long n, ptr st) {
     return fx_fake_quant_fwd(dt, CP(x), P(y), F(scale), bits, n, S(st));

@@ -17,7 +17,9 @@ def register_dataset(name, cls):
 
 def _register_optional():
     from .vision_dataset import GeneralClsDataset, ImageFolder, CIFAR, SyntheticImageDataset
-    for c in (GeneralClsDataset, ImageFolder, CIFAR, SyntheticImageDataset):
+    from .multimodal_dataset import ImagenDataset, SyntheticImagenDataset
+    for c in (GeneralClsDataset, ImageFolder, CIFAR, SyntheticImageDataset, ImagenDataset,
+              SyntheticImagenDataset):
         DATASETS[c.__name__] = c
 
 
