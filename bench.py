@@ -11,8 +11,12 @@ Config = BASELINE.json metric "tokens/sec (whole node) GPT-3 6.7B
 hybrid-parallel at 1/2/4/8 MI355X": h 4096, 32 layers, 32 heads, vocab
 50304, seq 1024, dropout 0.1 (as ``pretrain_gpt_6.7B_sharding16.yaml``), bf16
 compute with fp32 master weights, synthetic tokens, random-init weights.
-Layouts follow BASELINE.md: 1 GPU dp1, 2 tp2, 4 tp2*pp2, 8 tp2*pp2*dp2 (1F1B),
-weak scaling: 8 sequences x 1024 tokens of work per GPU per step.
+Layouts: chosen per GPU count by the MI355X layout planner
+(``fleetx_amd/parallel/auto/planner.py``: step-time model with per-link xGMI
+bandwidth, 1F1B bubble, ZeRO traffic and the 288 GB budget) unless
+``--layout dp,mp,pp,micro[,sharding[,stage]]`` pins one (e.g. the BASELINE
+TP2*PP2*DP2 config: ``--layout 2,2,2,2``).  Weak scaling: 8 sequences x 1024
+tokens of work per GPU per step.
 """
 import argparse
 import json
@@ -31,8 +35,6 @@ MODELS = {
 }
 PEAK_BF16 = 2.5e15  # MI355X dense bf16 (spec), per GPU
 
-# per-GPU count -> (dp, mp, pp, micro_batch)
-LAYOUTS = {1: (1, 1, 1, 8), 2: (1, 2, 1, 8), 4: (1, 2, 2, 2), 8: (2, 2, 2, 2)}
 
 
 def parse():
@@ -44,7 +46,8 @@ def parse():
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--per-gpu-seqs", type=int, default=8,
                     help="sequences of work per GPU per step (weak scaling)")
-    ap.add_argument("--layout", default=None, help="dp,mp,pp,micro override, e.g. 8,1,1,8")
+    ap.add_argument("--layout", default=None,
+                    help="dp,mp,pp,micro[,sharding[,stage]] override, e.g. 2,2,2,2")
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--sequence-parallel", action="store_true")
     ap.add_argument("--no-dropout", action="store_true")
@@ -69,14 +72,24 @@ def main():
             print("bench.py --gpus %d must be launched with torch.distributed.run" % args.gpus,
                   file=sys.stderr)
             sys.exit(2)
-    if args.layout:
-        dp, mp, pp, micro = [int(x) for x in args.layout.split(",")]
-    else:
-        dp, mp, pp, micro = LAYOUTS.get(n, (n, 1, 1, 8))
-    assert dp * mp * pp == n, "layout {} does not match {} GPUs".format((dp, mp, pp), n)
     h, L, a = MODELS[args.model]
     global_batch = args.per_gpu_seqs * n
-    local_batch = global_batch // dp
+    recompute = bool(args.recompute)
+    sharding, stage = 1, 1
+    if args.layout:
+        vals = [int(x) for x in args.layout.split(",")]
+        dp, mp, pp, micro = vals[:4]
+        sharding = vals[4] if len(vals) > 4 else 1
+        stage = vals[5] if len(vals) > 5 else 1
+    else:
+        from fleetx_amd.parallel.auto.planner import plan
+        p = plan(h, L, a, 50304, args.seq, global_batch, n)
+        dp, mp, pp, micro, sharding = p.dp, p.mp, p.pp, p.micro_batch, p.sharding
+        stage = max(1, p.sharding_stage)
+        recompute = recompute or p.recompute
+    assert dp * mp * pp * sharding == n, "layout {} does not match {} GPUs".format(
+        (dp, mp, pp, sharding), n)
+    local_batch = global_batch // (dp * sharding)
     micro = min(micro, local_batch)
     drop = 0.0 if args.no_dropout else 0.1
     here = os.path.dirname(os.path.abspath(__file__))
@@ -85,12 +98,14 @@ def main():
           "Model.num_attention_heads=%d" % a, "Model.vocab_size=50304",
           "Model.hidden_dropout_prob=%s" % drop, "Model.attention_probs_dropout_prob=%s" % drop,
           "Model.max_position_embeddings=%d" % max(1024, args.seq),
-          "Model.use_recompute=%s" % bool(args.recompute),
+          "Model.use_recompute=%s" % recompute,
           "Model.sequence_parallel=%s" % bool(args.sequence_parallel),
           "Global.local_batch_size=%d" % local_batch, "Global.micro_batch_size=%d" % micro,
           "Global.global_batch_size=None",
           "Distributed.dp_degree=%d" % dp, "Distributed.mp_degree=%d" % mp,
           "Distributed.pp_degree=%d" % pp,
+          "Distributed.sharding.sharding_degree=%d" % sharding,
+          "Distributed.sharding.sharding_stage=%d" % stage,
           "Engine.max_steps=%d" % (args.steps + args.warmup), "Engine.logging_freq=1000000",
           "Engine.save_load.save_steps=-1", "Engine.mix_precision.dtype=bfloat16",
           "Data.Train.dataset.max_seq_len=%d" % args.seq,
@@ -141,6 +156,9 @@ def main():
     tps = tokens / elapsed
     fpt = flops_per_token(module.gpt_config, S)
     mfu = tps * fpt / (n * PEAK_BF16)
+    par = "_".join(x for x in (
+        "dp%d" % dp if dp > 1 else "", "sharding%d_stage%d" % (sharding, stage) if sharding > 1
+        else "", "tp%d" % mp if mp > 1 else "", "pp%d" % pp if pp > 1 else "") if x) or "dp1"
     if env.get_rank() == 0:
         out = {
             "metric": "tokens/sec (whole node) GPT-3 6.7B hybrid-parallel at 1/2/4/8 MI355X"
@@ -150,8 +168,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16" if engine._dtype == torch.bfloat16 else str(engine._dtype).replace("torch.", ""), "data": "synthetic (random tokens), random-init weights",
             "config": {"model": args.model, "global_batch": global_batch, "seq_len": S,
-                       "parallelism": "dp%d_tp%d_pp%d" % (dp, mp, pp), "micro_batch": micro,
-                       "dropout": drop, "recompute": bool(args.recompute)},
+                       "parallelism": par, "micro_batch": micro,
+                       "dropout": drop, "recompute": recompute},
             "mfu": round(mfu, 4), "tokens_per_gpu": round(tps / n, 1),
             "final_loss": round(lval, 4),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)

@@ -273,31 +273,48 @@ def get_config(fname, overrides=None, show=False, nranks=None):
 # auto-parallel variants (reference config.py:332-464)
 # --------------------------------------------------------------------------
 def process_auto_dist_configs(config, nranks=None):
+    """Reference ``config.py:332-366``: ``dp = nranks / (mp * pp)`` and the
+    sharding degree must divide it.  The reference counts sharding ranks inside
+    dp; the hybrid topology here keeps sharding as its own axis, so the stored
+    ``dp_degree`` is the number of pure replicas (``dp / sharding``)."""
     dist = config.Distributed
     nranks = get_world_size() if nranks is None else nranks
     dist["mp_degree"] = dist.get("mp_degree") or 1
     dist["pp_degree"] = dist.get("pp_degree") or 1
-    dist.sharding["sharding_degree"] = dist.sharding.get("sharding_degree") or 1
+    sd = dist.sharding["sharding_degree"] = dist.sharding.get("sharding_degree") or 1
     other = dist.mp_degree * dist.pp_degree
     assert nranks % other == 0, "nranks should be divisible by mp_degree*pp_degree"
-    if not dist.get("dp_degree") or dist.dp_degree * other != nranks:
-        dist["dp_degree"] = nranks // other
-    assert dist.dp_degree % dist.sharding.sharding_degree == 0, \
-        "dp_degree must be divisible by sharding_degree"
+    data = nranks // other
+    if dist.get("dp_degree") and dist.dp_degree * other != nranks:
+        logger.warning("Mismatched config using {} cards with dp_degree[{}], mp_degree[{}], "
+                       "pp_degree[{}]; adjusting dp_degree to {}".format(
+                           nranks, dist.dp_degree, dist.mp_degree, dist.pp_degree, data))
+    if sd > data:  # e.g. sharding16 on a smaller node: shard over what exists
+        logger.warning("sharding_degree {} > data-parallel ranks {}; using {}".format(sd, data,
+                                                                                    data))
+        sd = dist.sharding["sharding_degree"] = data
+    assert data % sd == 0, "dp_degree[{}] must be divisible by sharding_degree[{}]".format(data, sd)
+    dist["dp_degree"] = data // sd
 
 
 def process_auto_global_configs(config):
-    dp = config.Distributed.dp_degree
+    d = config.Distributed
+    data = d.dp_degree * d.sharding.sharding_degree
     g = config.Global
     if g.global_batch_size is None and g.local_batch_size is None:
         raise ValueError("global_batch_size or local_batch_size should be set.")
     if g.global_batch_size is not None and g.local_batch_size is not None:
-        assert g.global_batch_size // g.local_batch_size == dp
-    elif g.global_batch_size is not None:
-        assert g.global_batch_size % dp == 0
-        g["local_batch_size"] = g.global_batch_size // dp
-    else:
-        g["global_batch_size"] = g.local_batch_size * dp
+        if g.global_batch_size // g.local_batch_size != data:
+            g["local_batch_size"] = None
+    if g.global_batch_size is not None and g.local_batch_size is None:
+        assert g.global_batch_size % data == 0, \
+            "global_batch_size[{}] should be divisible by data ranks[{}]".format(
+                g.global_batch_size, data)
+        g["local_batch_size"] = g.global_batch_size // data
+    elif g.global_batch_size is None:
+        g["global_batch_size"] = g.local_batch_size * data
+    if g.local_batch_size % g.micro_batch_size:
+        g["micro_batch_size"] = g.local_batch_size
     assert g.local_batch_size % g.micro_batch_size == 0
 
 
