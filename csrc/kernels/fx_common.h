@@ -92,18 +92,26 @@ __device__ __forceinline__ uint32_t elem_rand_pair(uint64_t i, uint32_t klo, uin
   return lowbias32((uint32_t)pair ^ c);
 }
 
+// Round-trip through the 16-bit storage type (what a store + reload would see).
+template <typename T>
+__device__ __forceinline__ float round_to(float f) {
+  return Elt<T>::to_f(Elt<T>::from_f(f));
+}
+
 // ---------------------------------------------------------------- math
+// tanh-GeLU via the identity 0.5 * (1 + tanh(u)) = 1 / (1 + exp(-2u)):
+// one v_exp_f32 + one v_rcp_f32 instead of libm tanhf's polynomial chain.
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
+  const float u = k0 * (x + k1 * x * x * x);
+  return x * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * u));
 }
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float x2 = x * x;
-  float u = k0 * (x + k1 * x2 * x);
-  float t = tanhf(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+  const float x2 = x * x;
+  const float u = k0 * (x + k1 * x2 * x);
+  const float s = __builtin_amdgcn_rcpf(1.f + __expf(-2.f * u));  // sigmoid(2u) = (1 + tanh u) / 2
+  return s + 2.f * x * s * (1.f - s) * k0 * (1.f + 3.f * k1 * x2);
 }
 __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));

@@ -69,8 +69,10 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
     }
     if (s_out) {
       store8<T>(s_out + base + c, v[i]);
-      // LN sees the value as stored (rounded) so fwd/bwd agree exactly.
-      load8<T>(s_out + base + c, v[i]);
+      // LN sees the value as stored (rounded) so fwd/bwd agree exactly; the
+      // rounding happens in registers (no dependent reload of the store).
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = round_to<T>(v[i][j]);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) sum += v[i][j];
@@ -135,7 +137,7 @@ __global__ __launch_bounds__(256) void add_ln_fwd_generic(
     value(vi * 8, v);
     if (s_out) {
       store8<T>(s_out + base + vi * 8, v);
-      load8<T>(s_out + base + vi * 8, v);
+      for (int j = 0; j < 8; ++j) v[j] = round_to<T>(v[j]);
     }
     for (int j = 0; j < 8; ++j) sum += v[j];
   }
@@ -385,9 +387,8 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(
       }
       store8<T>(dx + off, g);
       // accumulate the rounded value so dbias == colsum(dx) exactly
-      load8<T>(dx + off, g);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += g[j];
+      for (int j = 0; j < 8; ++j) acc[j] += round_to<T>(g[j]);
     }
   }
 #pragma unroll
@@ -455,7 +456,8 @@ __global__ __launch_bounds__(256) void dropout_bwd_colsum_kernel(
       for (int j = 0; j < 8; ++j) g[j] = drop_apply(g[j], off + j, drop);
       if (dx) {
         store8<T>(dx + off, g);
-        load8<T>(dx + off, g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = round_to<T>(g[j]);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += g[j];

@@ -144,19 +144,31 @@ class EagerEngine(BasicEngine):
         if mode == "train":
             comm = configs.Distributed.get("comm", {}) or {}
             sh_grp = self.hcg.get_sharding_parallel_group() if self._sharding_stage >= 1 else None
-            self.buffer = FlatParamGradBuffer(
-                model.named_parameters(), dp_group=self.hcg.get_data_parallel_group(),
-                shard_group=sh_grp if sh_grp is not None else self.hcg.get_sharding_parallel_group(),
-                mp_group=self.hcg.get_model_parallel_group(),
-                embed_group=self.hcg.get_embedding_group() if self.hcg.pp_degree > 1 else None,
-                bucket_mb=comm.get("dp_bucket_mb", 256),
-                overlap=comm.get("overlap_grad_reduce", True),
-                shard_stage=self._sharding_stage)
+            if self._sharding_stage == 3:
+                # reference: group_sharded_parallel(level='p_g_os') (eager_engine.py:228-242)
+                from ...parallel.sharding import Stage3ParamGradBuffer
+                assert self.hcg.pp_degree == 1, \
+                    "sharding stage 3 does not compose with pipeline parallelism"
+                self.buffer = Stage3ParamGradBuffer(
+                    model, shard_group=sh_grp, dp_group=self.hcg.get_data_parallel_group(),
+                    mp_group=self.hcg.get_model_parallel_group(),
+                    prefetch=comm.get("stage3_prefetch", True))
+            else:
+                self.buffer = FlatParamGradBuffer(
+                    model.named_parameters(), dp_group=self.hcg.get_data_parallel_group(),
+                    shard_group=sh_grp if sh_grp is not None
+                    else self.hcg.get_sharding_parallel_group(),
+                    mp_group=self.hcg.get_model_parallel_group(),
+                    embed_group=self.hcg.get_embedding_group() if self.hcg.pp_degree > 1 else None,
+                    bucket_mb=comm.get("dp_bucket_mb", 256),
+                    overlap=comm.get("overlap_grad_reduce", True),
+                    shard_stage=self._sharding_stage)
             if self.lr_scheduler is None and "lr" in configs.Optimizer:
                 self.lr_scheduler = build_lr_scheduler(configs.Optimizer.lr)
             self.optimizer = build_optimizer(configs.Optimizer, self.buffer, self.lr_scheduler,
                                              mp_group=self.hcg.get_model_parallel_group(),
-                                             pp_group=self.hcg.get_pipe_parallel_group())
+                                             pp_group=self.hcg.get_pipe_parallel_group(),
+                                             offload=bool(sh.get("sharding_offload", False)))
             if self._use_pure_fp16 and self._dtype == torch.float16:
                 self.scaler = DynamicLossScaler(amp.get("scale_loss", 32768.0), device=self.device)
                 self.optimizer.loss_scale = self.scaler.scale
@@ -178,7 +190,8 @@ class EagerEngine(BasicEngine):
 
     # ------------------------------------------------------------------ train
     def _fault_check(self, step):
-        if self._fault:
+        # only the first launch attempt faults, so a launcher restart can finish
+        if self._fault and os.environ.get("FLEETX_RESTART_COUNT", "0") == "0":
             r, s = self._fault.split(":")
             if int(r) == env.get_rank() and int(s) == step:
                 logger.error("fault injection: rank %s exits at step %s" % (r, s))
@@ -371,11 +384,18 @@ class EagerEngine(BasicEngine):
                                                          self._pp_rank))
         return base
 
+    def _params_gathered(self, writeback=False):
+        g = getattr(self.buffer, "gathered", None)
+        return g(writeback=writeback) if g is not None else contextlib.nullcontext()
+
     def save(self, epoch=0, step=0):
         if self._dp_rank != 0:
             return
         target = self._shard_dir(ckpt.step_dir(self._output_dir, epoch, step))
-        model_sd = {k: v.detach().cpu() for k, v in self._module.model.state_dict().items()}
+        # stage 3: gather full parameters first (reference get_all_parameters, :600-601)
+        with self._params_gathered():
+            model_sd = {k: v.detach().to("cpu", copy=True)
+                        for k, v in self._module.model.state_dict().items()}
         payloads = {"model.pdparams": model_sd}
         if self.optimizer is not None:
             payloads["model_state.pdopt"] = self.optimizer.state_dict()
@@ -405,7 +425,8 @@ class EagerEngine(BasicEngine):
         if not os.path.isfile(mp):
             raise FileNotFoundError("{} not found".format(mp))
         sd = ckpt.load_payload(mp)
-        self._module.model.load_state_dict(sd, strict=False)
+        with self._params_gathered(writeback=True):
+            self._module.model.load_state_dict(sd, strict=False)
         if self.mode == "train":
             op, mt = os.path.join(d, "model_state.pdopt"), os.path.join(d, "meta_state.pdopt")
             if not (os.path.isfile(op) and os.path.isfile(mt)):

@@ -41,11 +41,23 @@ def _sumsq(t):
     return (t.float() * t.float()).sum()
 
 
+_OFFLOAD_CHUNK = 1 << 25  # fp32 elements per streamed chunk (128 MiB per state tensor)
+
+
+def _host_copy(src16):
+    """fp32 pinned-host copy of a device range, converted chunk by chunk."""
+    host = torch.empty(src16.numel(), dtype=torch.float32, pin_memory=True)
+    for o in range(0, src16.numel(), _OFFLOAD_CHUNK):
+        host[o:o + _OFFLOAD_CHUNK].copy_(src16[o:o + _OFFLOAD_CHUNK].float())
+    return host
+
+
 class FlatOptimizer:
     """Base: owns master/state for the owned ranges of a flat buffer."""
 
     def __init__(self, learning_rate, buffer, grad_clip=None, weight_decay=0.0,
-                 multi_precision=True, check_group=None, pp_group=None, mp_group=None):
+                 multi_precision=True, check_group=None, pp_group=None, mp_group=None,
+                 offload=False):
         self._lr = learning_rate
         self.buffer = buffer
         self.grad_clip = grad_clip
@@ -55,7 +67,12 @@ class FlatOptimizer:
         self.pp_group = pp_group if pp_group is not None and pp_group.nranks > 1 else None
         self.step_count = 0
         dev = buffer.device
-        self.master = [buffer.param_flat[s:e].float().clone() for s, e, _ in self.ranges]
+        # sharding_offload: fp32 state lives in pinned host memory (GPU runs only)
+        self.offload = bool(offload) and dev.type == "cuda"
+        if self.offload:
+            self.master = [_host_copy(buffer.param_flat[s:e]) for s, e, _ in self.ranges]
+        else:
+            self.master = [buffer.param_flat[s:e].float().clone() for s, e, _ in self.ranges]
         self.found_inf = torch.zeros(1, dtype=torch.int32, device=dev)
         self.gscale = torch.ones(1, dtype=torch.float32, device=dev)
         self.last_grad_norm = torch.zeros((), dtype=torch.float32, device=dev)
@@ -138,8 +155,15 @@ class FlatOptimizer:
         raise NotImplementedError
 
     def refresh_master_from_params(self):
+        self.sync_state()
         for (s, e, _), m in zip(self.ranges, self.master):
             m.copy_(self.buffer.param_flat[s:e].float())
+
+    def sync_state(self):
+        """Host-offloaded state: wait for the last D2H copies to land."""
+        cs = getattr(self, "_copy_stream", None)
+        if cs is not None:
+            cs.synchronize()
 
 
 class FusedAdamW(FlatOptimizer):
@@ -152,15 +176,77 @@ class FusedAdamW(FlatOptimizer):
         tensor_fusion = kw.pop("tensor_fusion", None)  # always fused here
         del tensor_fusion
         super().__init__(learning_rate, buffer, grad_clip, weight_decay, multi_precision,
-                         kw.get("check_group"), kw.get("pp_group"), kw.get("mp_group"))
+                         kw.get("check_group"), kw.get("pp_group"), kw.get("mp_group"),
+                         offload=kw.get("offload", False))
         self.beta1, self.beta2, self.eps = float(beta1), float(beta2), float(epsilon)
-        self.m = [torch.zeros_like(x) for x in self.master]
-        self.v = [torch.zeros_like(x) for x in self.master]
+        if self.offload:
+            self.m = [torch.zeros(x.numel(), dtype=torch.float32, pin_memory=True)
+                      for x in self.master]
+            self.v = [torch.zeros(x.numel(), dtype=torch.float32, pin_memory=True)
+                      for x in self.master]
+            n = min(_OFFLOAD_CHUNK, max(e - s for s, e, _ in self.ranges))
+            dev = buffer.device
+            # two staging sets (master, m, v) so chunk j+1 uploads while j computes
+            self._stage = [[torch.empty(n, dtype=torch.float32, device=dev) for _ in range(3)]
+                           for _ in range(2)]
+            self._copy_stream = torch.cuda.Stream(device=dev)
+        else:
+            self.m = [torch.zeros_like(x) for x in self.master]
+            self.v = [torch.zeros_like(x) for x in self.master]
+
+    def _update_offloaded(self, lr, bc1, bc2):
+        """Stream host-resident master/m/v through the GPU in chunks: the H2D
+        copy of chunk j+1 and the D2H copy of chunk j-1 run on a copy stream
+        while the fused AdamW kernel updates chunk j (reference
+        ``group_sharded_parallel(offload=True)``, ``eager_engine.py:236-242``).
+        PCIe traffic: 24 B per parameter per step."""
+        k = _lib.kernels()
+        cur = torch.cuda.current_stream()
+        cs = self._copy_stream
+        pf = self.buffer.param_flat
+        gviews = self.grad_views()
+        jobs = [(ri, o, min(_OFFLOAD_CHUNK, (e - s) - o))
+                for ri, (s, e, _) in enumerate(self.ranges) for o in range(0, e - s, _OFFLOAD_CHUNK)]
+        if not jobs:
+            return
+        cs.wait_stream(cur)  # gscale / found_inf / grads are final
+
+        def upload(j):
+            ri, o, n = jobs[j]
+            with torch.cuda.stream(cs):
+                for host, dev in zip((self.master[ri], self.m[ri], self.v[ri]), self._stage[j % 2]):
+                    dev[:n].copy_(host[o:o + n], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(cs)
+            return ev
+
+        ready = upload(0)
+        for j, (ri, o, n) in enumerate(jobs):
+            nxt = upload(j + 1) if j + 1 < len(jobs) else None
+            s, e, c = self.ranges[ri]
+            wd = self.weight_decay if c.decay else 0.0
+            st = self._stage[j % 2]
+            cur.wait_event(ready)
+            k.adamw_flat(_lib.dt_code(pf.dtype), st[0].data_ptr(), gviews[ri][o:o + n].data_ptr(),
+                         st[1].data_ptr(), st[2].data_ptr(), pf[s + o:s + o + n].data_ptr(), n,
+                         float(lr), self.beta1, self.beta2, self.eps, float(wd), bc1, bc2,
+                         self.gscale.data_ptr(), self.found_inf.data_ptr(), _lib.stream())
+            done = torch.cuda.Event()
+            done.record(cur)
+            with torch.cuda.stream(cs):
+                cs.wait_event(done)
+                for host, dev in zip((self.master[ri], self.m[ri], self.v[ri]), st):
+                    host[o:o + n].copy_(dev[:n], non_blocking=True)
+            ready = nxt
 
     def _update(self, lr):
         t = self.step_count
         bc1 = 1.0 - self.beta1 ** t
         bc2 = 1.0 - self.beta2 ** t
+        if self.offload:
+            if not self.decoupled:
+                raise NotImplementedError("sharding_offload supports the decoupled AdamW family")
+            return self._update_offloaded(lr, bc1, bc2)
         pf = self.buffer.param_flat
         for (s, e, c), g, p, m, v in zip(self.ranges, self.grad_views(), self.master, self.m,
                                          self.v):
@@ -188,11 +274,14 @@ class FusedAdamW(FlatOptimizer):
                 out16.copy_(p)
 
     def state_dict(self):
-        return {"step": self.step_count, "master": [x.cpu() for x in self.master],
-                "m": [x.cpu() for x in self.m], "v": [x.cpu() for x in self.v],
+        self.sync_state()
+        cp = (lambda x: x.clone()) if self.offload else (lambda x: x.cpu())
+        return {"step": self.step_count, "master": [cp(x) for x in self.master],
+                "m": [cp(x) for x in self.m], "v": [cp(x) for x in self.v],
                 "lr": self._lr.state_dict() if hasattr(self._lr, "state_dict") else self._lr}
 
     def set_state_dict(self, state):
+        self.sync_state()
         self.step_count = state["step"]
         for dst, src in zip(self.master, state["master"]):
             dst.copy_(src)

@@ -1,0 +1,481 @@
+"""ZeRO stage 3: parameters, gradients and optimizer state all partitioned
+over the sharding group, with layer-granular gather / release.
+
+Capability parity: reference ``group_sharded_parallel(level='p_g_os')``
+reached from ``eager_engine.py:221-242`` (P06) and the save-time
+``get_all_parameters`` gather (``eager_engine.py:600-601``).
+
+MI355X design (not a translation of Paddle's GroupShardedStage3):
+
+* **Units.** Every repeated block (the children of the model's outermost
+  layer ``ModuleList`` -- one GPT decoder layer, one ViT block) is a *unit*;
+  everything else (embeddings, final norm, tied LM head) is the *root unit*.
+  A unit owns ONE full-size model-dtype flat buffer and ONE fp32 flat grad
+  buffer; its parameters are views into them.  Freeing a unit resizes the
+  two storages to zero bytes (the views stay valid and are re-backed by the
+  next gather) -- there is no per-parameter bookkeeping on the hot path.
+* **Segments.** Inside a unit parameters are grouped by optimizer category
+  (decay / tensor-parallel / sequence-parallel / norm-excluded) and each
+  category segment is padded to ``ALIGN * nshard``, so a rank's slice of a
+  segment is one contiguous piece.  The rank-local shard buffer is laid out
+  category-major across all units: the optimizer sees one contiguous range
+  per category (one fused AdamW launch each), exactly as for stage 1/2.
+* **Forward.** A unit's forward pre-hook waits for its gather (issued as a
+  prefetch by the previous unit) and immediately prefetches the next unit,
+  so the RCCL all-gather of layer i+1 overlaps the compute of layer i.  The
+  post-hook releases the unit and hooks the layer output, so the arrival of
+  its gradient re-gathers the unit right before the layer's backward (and
+  prefetches unit i-1).
+* **Backward.** Weight gradients land in the unit's fp32 grad buffer (the
+  fused-wgrad GEMM writes there directly).  When the last gradient of a unit
+  arrives its reduce-scatter is launched asynchronously and the full
+  parameters are released; the shard accumulation and the grad-buffer free
+  happen when the NEXT unit completes, so each reduce-scatter overlaps the
+  following layer's backward.
+* Peak per-rank memory: (params + grads + Adam state) / nshard plus two
+  layers of full parameters and fp32 grads in flight.
+"""
+import contextlib
+
+import torch
+import torch.distributed as dist
+
+from .grad_buffer import ALIGN, Category, _is_gloo, _round_up, default_decay_fn
+
+
+def _free(t):
+    if t.untyped_storage().size() != 0:
+        t.untyped_storage().resize_(0)
+
+
+def _alloc(t, numel):
+    nbytes = numel * t.element_size()
+    if t.untyped_storage().size() != nbytes:
+        t.untyped_storage().resize_(nbytes)
+
+
+def _in_backward():
+    try:
+        return torch._C._current_graph_task_id() != -1
+    except AttributeError:  # pragma: no cover - older torch
+        return False
+
+
+def _cat_order(k):
+    return (not k[0], not k[1], k[2], k[3])
+
+
+class _Segment:
+    __slots__ = ("cat", "fstart", "fend", "sstart", "send", "params")
+
+    def __init__(self, cat, fstart):
+        self.cat, self.fstart, self.fend = cat, fstart, fstart
+        self.sstart = self.send = 0
+        self.params = []  # (name, param, full offset)
+
+
+class _Unit:
+    def __init__(self, idx, module, named):
+        self.idx = idx
+        self.module = module
+        self.named = named
+        self.segments = []
+        self.numel = 0
+        self.full_param = None
+        self.full_grad = None
+        self.gathered = False
+        self.gather_works = []
+        self.grad_live = False
+        self.ready = 0
+        self.done = False
+        self.rs_pending = None  # (works, [(segment, reduced piece)])
+        self.shard_fresh = True  # shard grads not yet written this step
+
+
+def find_layer_units(model):
+    """Children of the shallowest ``nn.ModuleList`` holding >= 2 blocks."""
+    best = None
+    for name, mod in model.named_modules():
+        if isinstance(mod, torch.nn.ModuleList) and len(mod) >= 2:
+            depth = name.count(".")
+            if best is None or depth < best[0]:
+                best = (depth, mod)
+    return list(best[1]) if best is not None else []
+
+
+class Stage3ParamGradBuffer:
+    """Drop-in for :class:`FlatParamGradBuffer` when ``sharding_stage == 3``.
+
+    ``param_flat`` / ``grad_flat`` are the rank-local SHARDS (model dtype /
+    fp32); :meth:`owned_ranges` indexes into them, so the optimizers (and the
+    host-offloaded optimizer state) are unchanged.
+    """
+
+    def __init__(self, model, shard_group, dp_group=None, mp_group=None,
+                 decay_fn=default_decay_fn, prefetch=True, fused_wgrad=True):
+        assert shard_group is not None and shard_group.nranks > 1, "stage 3 needs sharding > 1"
+        self.shard_group = shard_group
+        self.shard_stage = 3
+        self.dp_group = dp_group if dp_group is not None and dp_group.nranks > 1 else None
+        self.mp_group = mp_group if mp_group is not None and mp_group.nranks > 1 else None
+        self.embed_group = None
+        self.prefetch = prefetch
+        self.nsh = shard_group.nranks
+        self.rank = shard_group.rank
+        self.gloo = _is_gloo(shard_group)
+        self._hooks = []
+        self._pending_rs = []
+
+        named_all = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        assert named_all, "no trainable parameters"
+        self.dtype = named_all[0][1].dtype
+        self.device = named_all[0][1].device
+        layer_mods = find_layer_units(model)
+        owner = {}
+        for li, m in enumerate(layer_mods):
+            for p in m.parameters():
+                owner.setdefault(id(p), li)
+        per_unit = [[] for _ in layer_mods]
+        root = []
+        for n, p in named_all:
+            if id(p) in owner:
+                per_unit[owner[id(p)]].append((n, p))
+            else:
+                root.append((n, p))
+        self.root = _Unit(-1, model, root) if root else None
+        self.units = []
+        for m, nm in zip(layer_mods, per_unit):
+            if nm:
+                self.units.append(_Unit(len(self.units), m, nm))
+        self.all_units = ([self.root] if self.root is not None else []) + self.units
+
+        # -- categories and per-unit full layout (segments padded to ALIGN*nsh)
+        self.categories = {}
+        for u in self.all_units:
+            segs = {}
+            for n, p in u.named:
+                key = (bool(decay_fn(n, p)), bool(getattr(p, "tp_split", False)),
+                       bool(getattr(p, "sequence_parallel", False)),
+                       bool(getattr(p, "norm_exclude", False)))
+                self.categories.setdefault(key, Category(key))
+                segs.setdefault(key, []).append((n, p))
+            off = 0
+            for key in sorted(segs, key=_cat_order):
+                seg = _Segment(self.categories[key], off)
+                for n, p in segs[key]:
+                    seg.params.append((n, p, off))
+                    off += _round_up(p.numel(), ALIGN)
+                off = _round_up(off, ALIGN * self.nsh)
+                seg.fend = off
+                u.segments.append(seg)
+            u.numel = off
+
+        # -- shard layout: category-major over all units
+        order = sorted(self.categories, key=_cat_order)
+        soff = 0
+        for key in order:
+            c = self.categories[key]
+            c.start = soff
+            for u in self.all_units:
+                for seg in u.segments:
+                    if seg.cat is c:
+                        piece = (seg.fend - seg.fstart) // self.nsh
+                        seg.sstart, seg.send = soff, soff + piece
+                        soff += piece
+            c.end = soff
+        self.category_list = [self.categories[k] for k in order]
+        self.numel = soff
+        self.param_flat = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
+        self.grad_flat = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+
+        # -- move parameters into full unit buffers, keep only this rank's shard
+        self.params = []
+        for u in self.all_units:
+            u.full_param = torch.zeros(u.numel, dtype=self.dtype, device=self.device)
+            u.full_grad = torch.zeros(u.numel, dtype=torch.float32, device=self.device)
+            for seg in u.segments:
+                for n, p, o in seg.params:
+                    view = u.full_param[o:o + p.numel()].view_as(p)
+                    view.copy_(p.data)
+                    p.data = view
+                    p.main_grad = u.full_grad[o:o + p.numel()].view_as(p)
+                    p.grad = None
+                    p._fx_fresh = True
+                    p._fx_fused_wgrad = bool(getattr(p, "_fx_fused_wgrad_ok", False)) and fused_wgrad
+                    p._fx_unit = u
+                    self.params.append((n, p))
+            u.gathered = True
+            u.grad_live = True
+            self._writeback_shard(u)
+            self._release_params(u)
+            self._release_grads(u)
+        self._install_hooks(model)
+
+    # ------------------------------------------------------------------ buffers
+    def _piece(self, seg):
+        return (seg.fend - seg.fstart) // self.nsh
+
+    def _writeback_shard(self, u):
+        for seg in u.segments:
+            piece = self._piece(seg)
+            lo = seg.fstart + self.rank * piece
+            self.param_flat[seg.sstart:seg.send].copy_(u.full_param[lo:lo + piece])
+
+    def _gather(self, u, async_op=True):
+        if u.gathered:
+            return
+        _alloc(u.full_param, u.numel)
+        works = []
+        for seg in u.segments:
+            out = u.full_param[seg.fstart:seg.fend]
+            mine = self.param_flat[seg.sstart:seg.send]
+            if self.gloo:
+                parts = [torch.empty_like(mine) for _ in range(self.nsh)]
+                dist.all_gather(parts, mine, group=self.shard_group.group)
+                out.copy_(torch.cat(parts))
+            else:
+                w = dist.all_gather_into_tensor(out, mine, group=self.shard_group.group,
+                                                async_op=async_op)
+                if w is not None:
+                    works.append(w)
+        u.gather_works = works
+        u.gathered = True
+
+    def _wait_gather(self, u):
+        for w in u.gather_works:
+            w.wait()
+        u.gather_works = []
+
+    def _release_params(self, u):
+        if not u.gathered:
+            return
+        self._wait_gather(u)
+        _free(u.full_param)
+        u.gathered = False
+
+    def _alloc_grads(self, u):
+        if u.grad_live:
+            return
+        _alloc(u.full_grad, u.numel)
+        u.grad_live = True
+        for seg in u.segments:
+            for n, p, o in seg.params:
+                p._fx_fresh = True
+        u.ready = 0
+        u.done = False
+
+    def _release_grads(self, u):
+        if u.grad_live:
+            _free(u.full_grad)
+            u.grad_live = False
+
+    # ------------------------------------------------------------------ hooks
+    def _install_hooks(self, model):
+        for u in self.units:
+            self._hooks.append(u.module.register_forward_pre_hook(self._make_pre_fwd(u)))
+            self._hooks.append(u.module.register_forward_hook(self._make_post_fwd(u)))
+        if self.root is not None:
+            self._hooks.append(model.register_forward_pre_hook(self._root_pre_fwd))
+        for n, p in self.params:
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._accum_hook))
+            p._fx_grad_ready = self._make_ready(p)
+
+    def _root_pre_fwd(self, module, args):
+        self._gather(self.root, async_op=False)
+        self._wait_gather(self.root)
+        if torch.is_grad_enabled():
+            self._alloc_grads(self.root)
+        if self.units and self.prefetch:
+            self._gather(self.units[0])
+
+    def _make_pre_fwd(self, u):
+        def hook(module, args):
+            self._gather(u)
+            self._wait_gather(u)
+            if self.prefetch and u.idx + 1 < len(self.units) and not _in_backward():
+                self._gather(self.units[u.idx + 1])
+        return hook
+
+    def _make_post_fwd(self, u):
+        def hook(module, args, output):
+            if _in_backward():  # a module-level re-forward inside backward keeps the params
+                return output
+            if torch.is_grad_enabled():
+                outs = output if isinstance(output, (tuple, list)) else (output,)
+                fired = [False]
+
+                def pre_bwd(grad, u=u, fired=fired):
+                    if not fired[0]:
+                        fired[0] = True
+                        self._pre_backward(u)
+                    return grad
+                for t in outs:
+                    if torch.is_tensor(t) and t.requires_grad:
+                        t.register_hook(pre_bwd)
+            self._release_params(u)
+            return output
+        return hook
+
+    def _pre_backward(self, u):
+        self._gather(u)
+        self._wait_gather(u)
+        self._alloc_grads(u)
+        if self.prefetch and u.idx >= 1:
+            self._gather(self.units[u.idx - 1])
+
+    def _accum_hook(self, param):
+        g = param.grad
+        if g is None:  # fused-wgrad Functions already wrote main_grad
+            return
+        if param._fx_fresh:
+            param.main_grad.copy_(g)
+        else:
+            param.main_grad.add_(g)
+        param._fx_fresh = False
+        param.grad = None
+        param._fx_grad_ready()
+
+    def _make_ready(self, p):
+        def ready():
+            u = p._fx_unit
+            if u is self.root:  # root grads are reduced once, in finish()
+                return
+            u.ready += 1
+            if u.ready == len(u.named):
+                self._unit_backward_done(u)
+        return ready
+
+    # ------------------------------------------------------------------ reduce-scatter
+    def _zero_missing(self, u):
+        """Params that got no gradient and the alignment gaps must not carry
+        stale memory into the reduction."""
+        for seg in u.segments:
+            prev = seg.fstart
+            for n, p, o in seg.params:
+                if p._fx_fresh:
+                    p.main_grad.zero_()
+                    p._fx_fresh = False
+                if o > prev:
+                    u.full_grad[prev:o].zero_()
+                prev = o + p.numel()
+            if seg.fend > prev:
+                u.full_grad[prev:seg.fend].zero_()
+
+    def _launch_rs(self, u):
+        self._zero_missing(u)
+        works, pieces = [], []
+        for seg in u.segments:
+            full = u.full_grad[seg.fstart:seg.fend]
+            piece = self._piece(seg)
+            if self.gloo:
+                dist.all_reduce(full, group=self.shard_group.group)
+                red = full[self.rank * piece:(self.rank + 1) * piece]
+            else:
+                red = torch.empty(piece, dtype=torch.float32, device=self.device)
+                works.append(dist.reduce_scatter_tensor(red, full, group=self.shard_group.group,
+                                                        async_op=True))
+            pieces.append((seg, red))
+        u.rs_pending = (works, pieces)
+        u.done = True
+
+    def _complete_rs(self, u):
+        if u.rs_pending is None:
+            return
+        works, pieces = u.rs_pending
+        for w in works:
+            w.wait()
+        for seg, red in pieces:
+            dst = self.grad_flat[seg.sstart:seg.send]
+            if u.shard_fresh:
+                dst.copy_(red)
+            else:
+                dst.add_(red)
+        u.shard_fresh = False
+        u.rs_pending = None
+        self._release_grads(u)
+
+    def _drain(self):
+        while self._pending_rs:
+            self._complete_rs(self._pending_rs.pop(0))
+
+    def _unit_backward_done(self, u):
+        if u.done:
+            return
+        self._launch_rs(u)
+        self._release_params(u)
+        # the previous unit's reduce-scatter overlapped this unit's backward
+        self._drain()
+        self._pending_rs.append(u)
+
+    # ------------------------------------------------------------------ engine API
+    def set_last_micro_batch(self, last):
+        self._drain()
+        for u in self.units:
+            u.ready = 0
+            u.done = False
+
+    def zero_grad(self):
+        for u in self.all_units:
+            u.shard_fresh = True
+
+    def finish(self):
+        """Complete every reduction; average over the data world."""
+        for u in self.units:
+            if u.grad_live and not u.done:  # backward never reached every param
+                self._launch_rs(u)
+                self._pending_rs.append(u)
+        if self.root is not None and self.root.grad_live:
+            self._launch_rs(self.root)
+            self._pending_rs.append(self.root)
+        self._drain()
+        for u in self.all_units:
+            if u.shard_fresh:  # no gradient at all this step
+                for seg in u.segments:
+                    self.grad_flat[seg.sstart:seg.send].zero_()
+                u.shard_fresh = False
+            self._release_params(u)
+        data_world = self.nsh
+        if self.dp_group is not None:
+            dist.all_reduce(self.grad_flat, group=self.dp_group.group)
+            data_world *= self.dp_group.nranks
+        self.grad_flat.mul_(1.0 / data_world)
+        if self.mp_group is not None:
+            for c in self.category_list:
+                if c.seq_parallel and c.end > c.start:
+                    dist.all_reduce(self.grad_flat[c.start:c.end], group=self.mp_group.group)
+
+    def owned_ranges(self):
+        return [(c.start, c.end, c) for c in self.category_list]
+
+    def allgather_params(self):
+        """No-op: parameters are gathered lazily by the next forward."""
+
+    @contextlib.contextmanager
+    def gathered(self, writeback=False):
+        """Materialise every full parameter (checkpoint save / load / export).
+        With ``writeback`` the (possibly loaded) full values are copied back
+        into this rank's shard before release."""
+        for u in self.all_units:
+            self._gather(u, async_op=False)
+            self._wait_gather(u)
+        try:
+            yield
+        finally:
+            for u in self.all_units:
+                if writeback:
+                    self._writeback_shard(u)
+                self._release_params(u)
+
+    def memory_report(self):
+        """Bytes resident per rank (shards) vs. what an unsharded layout holds."""
+        full = sum(u.numel for u in self.all_units)
+        esz = self.param_flat.element_size()
+        return {"shard_param_bytes": self.param_flat.numel() * esz,
+                "shard_grad_bytes": self.grad_flat.numel() * 4,
+                "unsharded_param_bytes": full * esz,
+                "unsharded_grad_bytes": full * 4}
+
+    def remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

@@ -234,6 +234,42 @@ def test_fused_adamw_matches_torch():
     assert _rel(lin.bias, ref.bias) < 1e-2
 
 
+def test_offloaded_adamw_matches_resident():
+    """sharding_offload: host-pinned fp32 state streamed through the GPU in
+    chunks gives bit-identical updates to the device-resident optimizer."""
+    from fleetx_amd.parallel.grad_buffer import FlatParamGradBuffer
+    from fleetx_amd.optims import optimizer as O
+    torch.manual_seed(3)
+    old = O._OFFLOAD_CHUNK
+    O._OFFLOAD_CHUNK = 4096  # force many chunks / both staging buffers
+    try:
+        mods, opts, bufs = [], [], []
+        for off in (False, True):
+            torch.manual_seed(3)
+            m = torch.nn.Sequential(torch.nn.Linear(128, 192), torch.nn.Linear(192, 64)).cuda()
+            m = m.bfloat16()
+            b = FlatParamGradBuffer(m.named_parameters())
+            o = O.FusedAdamW(1e-2, b, grad_clip=O.ClipGradByGlobalNorm(0.5), weight_decay=0.1,
+                             offload=off)
+            assert o.offload == off
+            mods.append(m), opts.append(o), bufs.append(b)
+        for step in range(3):
+            x = torch.randn(32, 128, device=DEV, dtype=torch.bfloat16)
+            for m, o, b in zip(mods, opts, bufs):
+                m(x).float().pow(2).mean().backward()
+                b.finish()
+                o.step()
+                o.clear_grad()
+        torch.cuda.synchronize()
+        for (_, p0), (_, p1) in zip(mods[0].named_parameters(), mods[1].named_parameters()):
+            assert torch.equal(p0, p1)
+        s0, s1 = opts[0].state_dict(), opts[1].state_dict()
+        for a, b in zip(s0["m"], s1["m"]):
+            assert torch.equal(a.cpu(), b.cpu())
+    finally:
+        O._OFFLOAD_CHUNK = old
+
+
 def test_fake_quant():
     from fleetx_amd.ops import quant
     x = torch.randn(1000, device=DEV, dtype=torch.bfloat16)

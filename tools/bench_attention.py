@@ -1,0 +1,60 @@
+"""Fused attention micro-benchmark on MI355X (forward and backward, causal /
+non-causal, attention dropout on / off) at the GPT-3 6.7B training shape.
+
+Prints one JSON line per case with milliseconds and achieved TFLOP/s
+(forward 4*B*H*S^2*D, backward 2.5x that, both halved when causal -- the
+useful FLOPs, not what a kernel happens to execute).
+
+    python tools/bench_attention.py [--b 8 --s 1024 --h 32 --d 128 --iters 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), "..")))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--b", type=int, default=8)
+    ap.add_argument("--s", type=int, default=1024)
+    ap.add_argument("--h", type=int, default=32)
+    ap.add_argument("--d", type=int, default=128)
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    from fleetx_amd import ops
+    B, S, H, D = args.b, args.s, args.h, args.d
+    qkv = torch.randn(B, S, H, 3, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    g = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+    for causal in (True, False):
+        for p in (0.0, 0.1):
+            def fwd():
+                return ops.flash_attention_qkvpacked(qkv, causal=causal, dropout_p=p, key=12345)
+            for _ in range(3):
+                torch.autograd.grad(fwd(), qkv, g)
+            torch.cuda.synchronize()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            tf = tb = 0.0
+            for _ in range(args.iters):
+                ev[0].record()
+                o = fwd()
+                ev[1].record()
+                torch.autograd.grad(o, qkv, g)
+                ev[2].record()
+                torch.cuda.synchronize()
+                tf += ev[0].elapsed_time(ev[1])
+                tb += ev[1].elapsed_time(ev[2])
+            tf /= args.iters
+            tb /= args.iters
+            flops = 4.0 * B * H * S * S * D * (0.5 if causal else 1.0)
+            print(json.dumps({"B": B, "S": S, "H": H, "D": D, "causal": causal, "dropout": p,
+                              "fwd_ms": round(tf, 4), "bwd_ms": round(tb, 4),
+                              "fwd_tflops": round(flops / tf / 1e9, 1),
+                              "bwd_tflops": round(2.5 * flops / tb / 1e9, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
