@@ -172,6 +172,10 @@ class EagerEngine(BasicEngine):
             if self._use_pure_fp16 and self._dtype == torch.float16:
                 self.scaler = DynamicLossScaler(amp.get("scale_loss", 32768.0), device=self.device)
                 self.optimizer.loss_scale = self.scaler.scale
+            # step N's AdamW runs on a side stream under step N+1's forward
+            if comm.get("overlap_optimizer", True) and not self._pipeline \
+                    and self.scaler is None and hasattr(self.optimizer, "enable_forward_overlap"):
+                self.optimizer.enable_forward_overlap(model)
             if self._pipeline:
                 model.attach(self)
         self._profiler = self._build_profiler(configs.get("Profiler"))
@@ -391,6 +395,8 @@ class EagerEngine(BasicEngine):
     def save(self, epoch=0, step=0):
         if self._dp_rank != 0:
             return
+        if self.optimizer is not None:
+            self.optimizer.sync_state()  # an overlapped update may still be in flight
         target = self._shard_dir(ckpt.step_dir(self._output_dir, epoch, step))
         # stage 3: gather full parameters first (reference get_all_parameters, :600-601)
         with self._params_gathered():
@@ -414,7 +420,12 @@ class EagerEngine(BasicEngine):
         if not ckpt_dir:
             return
         if ckpt_dir == "auto":
-            ckpt_dir = ckpt.latest_checkpoint(self._output_dir)
+            shards = None
+            if self._distributed:
+                h = self.hcg
+                shards = [ckpt.shard_dirname(m, s, p) for m in range(h.mp_degree)
+                          for s in range(h.sharding_degree) for p in range(h.pp_degree)]
+            ckpt_dir = ckpt.latest_checkpoint(self._output_dir, shards)
             if ckpt_dir is None:
                 logger.info("no checkpoint to resume from in %s" % self._output_dir)
                 return

@@ -135,10 +135,68 @@ class FlatOptimizer:
 
     # ------------------------------------------------------------------ API
     def step(self):
+        self._join_overlap()
         self._prepare_scale()
         self.step_count += 1
         self._update(self.get_lr())
         self.buffer.allgather_params()
+
+    # ------------------------------------------------------------------ overlap
+    _overlap_groups = None
+
+    def enable_forward_overlap(self, model):
+        """Run the parameter update of step N on a side stream, unit by unit
+        in FORWARD order, and let step N+1's forward start immediately: each
+        layer's forward pre-hook waits only for ITS parameters' update.
+
+        The update is HBM-bound (~30 B per parameter) while the forward is
+        GEMM-bound, so the two share the GPU instead of serialising.  Needs
+        device-resident state over an unsharded flat buffer (ZeRO stage 0);
+        returns False (and changes nothing) otherwise."""
+        from ..parallel.sharding import find_layer_units
+        buf = self.buffer
+        if (buf.device.type != "cuda" or self.offload or getattr(buf, "shard_stage", 0) != 0
+                or not hasattr(buf, "offsets")):
+            return False
+        units = find_layer_units(model)
+        if not units:
+            return False
+        owner = {}
+        for i, m in enumerate(units):
+            for p in m.parameters():
+                owner.setdefault(id(p), i)
+        groups = {}
+        for ri, (s, e, c) in enumerate(self.ranges):
+            items = sorted((buf.offsets[id(p)][0], owner.get(id(p), -1)) for _, p in c.params)
+            cur_u, lo = None, s
+            for off, u in items:
+                if cur_u is None:
+                    cur_u = u
+                elif u != cur_u:
+                    groups.setdefault(cur_u, []).append((ri, lo, off))
+                    cur_u, lo = u, off
+            if cur_u is not None:
+                groups.setdefault(cur_u, []).append((ri, lo, e))
+        self._overlap_groups = [(u, groups[u]) for u in sorted(groups)]  # root (-1) first
+        self._opt_stream = torch.cuda.Stream(device=buf.device)
+        self._unit_events = {}
+        self._overlap_hooks = [model.register_forward_pre_hook(self._make_wait(-1))]
+        for i, m in enumerate(units):
+            self._overlap_hooks.append(m.register_forward_pre_hook(self._make_wait(i)))
+        return True
+
+    def _make_wait(self, unit):
+        def hook(module, args):
+            ev = self._unit_events.pop(unit, None)
+            if ev is not None:
+                torch.cuda.current_stream().wait_event(ev)
+        return hook
+
+    def _join_overlap(self):
+        """Order the current stream after every pending overlapped update."""
+        if self._overlap_groups is not None:
+            torch.cuda.current_stream().wait_stream(self._opt_stream)
+            self._unit_events.clear()
 
     def clear_grad(self, set_to_zero=True):
         self.buffer.zero_grad()
@@ -160,7 +218,9 @@ class FlatOptimizer:
             m.copy_(self.buffer.param_flat[s:e].float())
 
     def sync_state(self):
-        """Host-offloaded state: wait for the last D2H copies to land."""
+        """Wait for the last update: host-offloaded D2H copies, or the
+        forward-overlapped update stream."""
+        self._join_overlap()
         cs = getattr(self, "_copy_stream", None)
         if cs is not None:
             cs.synchronize()
@@ -193,6 +253,31 @@ class FusedAdamW(FlatOptimizer):
         else:
             self.m = [torch.zeros_like(x) for x in self.master]
             self.v = [torch.zeros_like(x) for x in self.master]
+
+    def _update_overlapped(self, lr, bc1, bc2):
+        """AdamW per unit (root first, then layer 0, 1, ...) on the side
+        stream; an event per unit gates that unit's next forward."""
+        k = _lib.kernels()
+        pf = self.buffer.param_flat
+        gf = self.buffer.grad_flat
+        dt = _lib.dt_code(pf.dtype)
+        os_ = self._opt_stream
+        os_.wait_stream(torch.cuda.current_stream())  # grads final, clip scale computed
+        with torch.cuda.stream(os_):
+            st = _lib.stream()
+            for u, pieces in self._overlap_groups:
+                for ri, lo, hi in pieces:
+                    s, e, c = self.ranges[ri]
+                    wd = self.weight_decay if c.decay else 0.0
+                    a, b = lo - s, hi - s
+                    k.adamw_flat(dt, self.master[ri][a:b].data_ptr(), gf[lo:hi].data_ptr(),
+                                 self.m[ri][a:b].data_ptr(), self.v[ri][a:b].data_ptr(),
+                                 pf[lo:hi].data_ptr(), hi - lo, float(lr), self.beta1, self.beta2,
+                                 self.eps, float(wd), bc1, bc2, self.gscale.data_ptr(),
+                                 self.found_inf.data_ptr(), st)
+                ev = torch.cuda.Event()
+                ev.record(os_)
+                self._unit_events[u] = ev
 
     def _update_offloaded(self, lr, bc1, bc2):
         """Stream host-resident master/m/v through the GPU in chunks: the H2D
@@ -247,6 +332,8 @@ class FusedAdamW(FlatOptimizer):
             if not self.decoupled:
                 raise NotImplementedError("sharding_offload supports the decoupled AdamW family")
             return self._update_offloaded(lr, bc1, bc2)
+        if self._overlap_groups is not None and self.decoupled:
+            return self._update_overlapped(lr, bc1, bc2)
         pf = self.buffer.param_flat
         for (s, e, c), g, p, m, v in zip(self.ranges, self.grad_views(), self.master, self.m,
                                          self.v):

@@ -44,18 +44,32 @@ def load_payload(path, map_location="cpu"):
     return torch.load(path, map_location=map_location, weights_only=True)
 
 
-def latest_checkpoint(output_dir):
-    """Most recent ``epoch_E_step_S`` directory (for automatic resume)."""
+def _complete(step_path, shards):
+    """Every expected shard directory has its meta file (written last)."""
+    if not shards:
+        return os.path.isfile(os.path.join(step_path, "meta_state.pdopt")) or any(
+            os.path.isfile(os.path.join(step_path, d, "meta_state.pdopt"))
+            for d in os.listdir(step_path) if d.startswith("mp_"))
+    return all(os.path.isfile(os.path.join(step_path, d, "meta_state.pdopt")) for d in shards)
+
+
+def latest_checkpoint(output_dir, shards=None):
+    """Most recent COMPLETE ``epoch_E_step_S`` directory (automatic resume).
+
+    ``shards``: the shard directory names every (mp, sharding, pp) rank
+    writes; a step directory missing any of them (a crash mid-save) is
+    skipped in favour of the previous one."""
     if not os.path.isdir(output_dir):
         return None
-    best, best_key = None, None
+    cands = []
     for d in os.listdir(output_dir):
         if d.startswith("epoch_") and "_step_" in d and ".tmp" not in d:
             try:
                 e, s = d[len("epoch_"):].split("_step_")
-                key = (int(e), int(s))
+                cands.append(((int(e), int(s)), os.path.join(output_dir, d)))
             except ValueError:
                 continue
-            if best_key is None or key > best_key:
-                best, best_key = os.path.join(output_dir, d), key
-    return best
+    for _, path in sorted(cands, reverse=True):
+        if _complete(path, shards):
+            return path
+    return None

@@ -1,0 +1,6 @@
+#!/bin/bash
+# GPT-345M semi-auto parallel, one card
+# Recipe parity: reference projects/gpt/auto_gpt_345M_single_card.sh
+set -e
+cd "$(dirname "$0")/../.."
+python tools/auto.py -c fleetx_amd/configs/nlp/gpt/auto/pretrain_gpt_345M_single_card.yaml "$@"

@@ -1,0 +1,6 @@
+#!/bin/bash
+# GPT-1.3B pretraining on one MI355X
+# Recipe parity: reference projects/gpt/pretrain_gpt_1.3B_single_card.sh
+set -e
+cd "$(dirname "$0")/../.."
+python tools/train.py -c fleetx_amd/configs/nlp/gpt/pretrain_gpt_1.3B_single_card.yaml "$@"

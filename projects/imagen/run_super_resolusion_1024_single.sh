@@ -1,0 +1,6 @@
+#!/bin/bash
+# Imagen super-resolution 1024, one card
+# Recipe parity: reference projects/imagen/run_super_resolusion_1024_single.sh
+set -e
+cd "$(dirname "$0")/../.."
+python tools/train.py -c fleetx_amd/configs/multimodal/imagen/imagen_super_resolusion_1024.yaml "$@"

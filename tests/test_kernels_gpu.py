@@ -270,6 +270,43 @@ def test_offloaded_adamw_matches_resident():
         O._OFFLOAD_CHUNK = old
 
 
+def test_forward_overlapped_adamw_matches_serial():
+    """Step N's update on a side stream, gated per layer by the next forward,
+    reproduces the serial update exactly."""
+    from fleetx_amd.models.language_model.gpt.model import (GPTConfig, GPTForPretraining,
+                                                            GPTPretrainingCriterion)
+    from fleetx_amd.parallel.grad_buffer import FlatParamGradBuffer
+    from fleetx_amd.optims.optimizer import FusedAdamW, ClipGradByGlobalNorm
+    runs = []
+    for overlap in (False, True):
+        torch.manual_seed(0)
+        cfg = GPTConfig(vocab_size=1024, hidden_size=256, num_layers=3, num_attention_heads=4,
+                        max_position_embeddings=128, hidden_dropout_prob=0.0,
+                        attention_probs_dropout_prob=0.0, dtype=torch.bfloat16)
+        model = GPTForPretraining(cfg).cuda()
+        crit = GPTPretrainingCriterion(cfg)
+        buf = FlatParamGradBuffer(model.named_parameters())
+        opt = FusedAdamW(1e-3, buf, grad_clip=ClipGradByGlobalNorm(1.0), weight_decay=0.01)
+        if overlap:
+            assert opt.enable_forward_overlap(model)
+            assert len(opt._overlap_groups) == 4  # root + 3 layers
+        g = torch.Generator(device=DEV).manual_seed(5)
+        losses = []
+        for _ in range(4):
+            toks = torch.randint(0, 1024, (4, 129), device=DEV, generator=g)
+            loss = crit(model(toks[:, :-1]), toks[:, 1:], torch.ones(4, 128, device=DEV))
+            loss.backward()
+            buf.finish()
+            opt.step()
+            opt.clear_grad()
+            losses.append(loss.detach())
+        opt.sync_state()
+        runs.append(([l.item() for l in losses], [p.detach().clone() for p in model.parameters()]))
+    assert runs[0][0] == runs[1][0], (runs[0][0], runs[1][0])
+    for a, b in zip(runs[0][1], runs[1][1]):
+        assert torch.equal(a, b)
+
+
 def test_fake_quant():
     from fleetx_amd.ops import quant
     x = torch.randn(1000, device=DEV, dtype=torch.bfloat16)
