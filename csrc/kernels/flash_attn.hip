@@ -100,7 +100,51 @@ struct Glds {
   }
 };
 
+// Same loads with the per-lane part of the address (row * stride + swizzled
+// chunk) computed ONCE per kernel: a full tile then costs one wave-uniform
+// scalar offset plus one 64-bit add per instruction instead of a 64-bit
+// multiply chain per lane per tile.  Partial (tail) tiles take the clamping
+// path above.
+template <int D, int ROWS>
+struct GldsStream {
+  using G = Glds<D, ROWS>;
+  const uint16_t* base;
+  long stride;
+  int nvalid, w;
+  long off[G::NI];
+  __device__ __forceinline__ void init(const uint16_t* b, long s, int nv, int wave, int lane) {
+    base = b;
+    stride = s;
+    nvalid = nv;
+    w = wave;
+#pragma unroll
+    for (int u = 0; u < G::NI; ++u) {
+      const int lin = (w * G::NI + u) * 1024 + lane * 16;
+      const int row = lin / G::RB, chp = (lin % G::RB) >> 4;
+      off[u] = (long)row * stride + (chp ^ swz<D>(row)) * 8;
+    }
+  }
+  __device__ __forceinline__ void load(int row0, char* tile, int lane) const {
+    if (row0 + ROWS > nvalid) {
+      G::load(base, stride, row0, nvalid, tile, w, lane);
+      return;
+    }
+    const uint16_t* tb = base + (long)row0 * stride;
+#pragma unroll
+    for (int u = 0; u < G::NI; ++u)
+      __builtin_amdgcn_global_load_lds((const void*)(tb + off[u]),
+                                       (__attribute__((address_space(3))) void*)(
+                                           tile + (w * G::NI + u) * 1024),
+                                       16, 0, 0);
+  }
+};
+
 __device__ __forceinline__ void glds_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// exp2 on the hardware unit (v_exp_f32): the inputs here are <= 0 after the
+// row max is subtracted, and flushing results below 2^-126 to zero is exact
+// enough for softmax -- libm exp2f adds a denormal-range fix-up per element.
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 struct AttnParams {
   const uint16_t *q, *k, *v, *o, *dout;
@@ -189,9 +233,12 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
   const float sl2 = P.scale * LOG2E;
   const uint32_t cb = DROP ? (lowbias32((uint32_t)bh ^ P.khi) ^ P.klo) : 0u;
 
+  GldsStream<D, KV> kld, vld;
+  kld.init(kp, P.sk_s, kv_end, w, lane);
+  vld.init(vp, P.sv_s, kv_end, w, lane);
   if (ntiles > 0) {
-    Glds<D, KV>::load(kp, P.sk_s, 0, kv_end, smem, w, lane);
-    Glds<D, KV>::load(vp, P.sv_s, 0, kv_end, smem + 2 * TB, w, lane);
+    kld.load(0, smem, lane);
+    vld.load(0, smem + 2 * TB, lane);
   }
   glds_wait();
   __syncthreads();
@@ -202,20 +249,25 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
     const char* vt = smem + 2 * TB + cur * TB;
     const bool more = it + 1 < ntiles;
     if (more) {
-      Glds<D, KV>::load(kp, P.sk_s, (it + 1) * KV, kv_end, smem + (cur ^ 1) * TB, w, lane);
-      Glds<D, KV>::load(vp, P.sv_s, (it + 1) * KV, kv_end, smem + 2 * TB + (cur ^ 1) * TB, w,
-                        lane);
+      kld.load((it + 1) * KV, smem + (cur ^ 1) * TB, lane);
+      vld.load((it + 1) * KV, smem + 2 * TB + (cur ^ 1) * TB, lane);
     }
     const int kb = it * KV;
     if (!(CAUSAL && kb > wq0 + 31)) {
       floatx16 sacc[2];
+      // all K fragments of the tile up front: the 16 LDS reads overlap each
+      // other instead of one exposed LDS latency per MFMA
+      bf16x8 kfr[2][D / 16];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s) kfr[t][s] = row_frag<D>(kt, 32 * t + (lane & 31), s, h);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) sacc[t][i] = 0.f;
 #pragma unroll
-        for (int s = 0; s < D / 16; ++s)
-          sacc[t] = mfma(row_frag<D>(kt, 32 * t + (lane & 31), s, h), qf[s], sacc[t]);
+        for (int s = 0; s < D / 16; ++s) sacc[t] = mfma(kfr[t][s], qf[s], sacc[t]);
       }
       const bool need_mask = (CAUSAL && kb + KV - 1 > wq0) || (kb + KV > kv_len);
       float mloc = -INFINITY;
@@ -235,18 +287,22 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
       mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
       const float m_new = fmaxf(m_run, mloc);
       const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-      const float alpha = exp2f(m_run - m_use);
+      const float alpha = fexp2(m_run - m_use);
       m_run = m_new;
       lsum *= alpha;
+      // once every row max of the wave is settled alpha == 1 exactly: skip
+      // the 64-register rescale (wave-uniform branch)
+      if (__any(alpha != 1.f)) {
 #pragma unroll
-      for (int dt = 0; dt < D / 32; ++dt)
+        for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+          for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+      }
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int i = 0; i < 16; i += 2) {
-          float p0 = exp2f(sacc[t][i] - m_use), p1 = exp2f(sacc[t][i + 1] - m_use);
+          float p0 = fexp2(sacc[t][i] - m_use), p1 = fexp2(sacc[t][i + 1] - m_use);
           lsum += p0 + p1;
           if (DROP) {
             const int key = kb + 32 * t + crow(i, h);  // even
@@ -371,9 +427,12 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) dqacc[dt][i] = 0.f;
 
+  GldsStream<D, KV> kld, vld;
+  kld.init(kp, P.sk_s, kv_end, w, lane);
+  vld.init(vp, P.sv_s, kv_end, w, lane);
   if (ntiles > 0) {
-    Glds<D, KV>::load(kp, P.sk_s, 0, kv_end, smem, w, lane);
-    Glds<D, KV>::load(vp, P.sv_s, 0, kv_end, smem + 2 * TB, w, lane);
+    kld.load(0, smem, lane);
+    vld.load(0, smem + 2 * TB, lane);
   }
   glds_wait();
   __syncthreads();
@@ -384,9 +443,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
     const char* vt = smem + 2 * TB + cur * TB;
     const bool more = it + 1 < ntiles;
     if (more) {
-      Glds<D, KV>::load(kp, P.sk_s, (it + 1) * KV, kv_end, smem + (cur ^ 1) * TB, w, lane);
-      Glds<D, KV>::load(vp, P.sv_s, (it + 1) * KV, kv_end, smem + 2 * TB + (cur ^ 1) * TB, w,
-                        lane);
+      kld.load((it + 1) * KV, smem + (cur ^ 1) * TB, lane);
+      vld.load((it + 1) * KV, smem + 2 * TB + (cur ^ 1) * TB, lane);
     }
     const int kb = it * KV;
     if (!(CAUSAL && kb > wq0 + 31)) {
@@ -406,7 +464,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
         for (int i = 0; i < 16; i += 2) {
           const int key = kb + 32 * t + crow(i, h);
           const float sc = KB ? 1.f : sl2;
-          float p0 = exp2f(sacc[i] * sc - lse2), p1 = exp2f(sacc[i + 1] * sc - lse2);
+          float p0 = fexp2(sacc[i] * sc - lse2), p1 = fexp2(sacc[i + 1] * sc - lse2);
           if (need_mask) {
             if ((CAUSAL && key > qi) || key >= kv_len) p0 = 0.f;
             if ((CAUSAL && key + 1 > qi) || key + 1 >= kv_len) p1 = 0.f;
@@ -451,20 +509,29 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
   }
 }
 
+// swap a 32-bit value with the neighbouring lane (lane ^ 1) through DPP
+__device__ __forceinline__ uint32_t dpp_swap1(uint32_t v) {
+  // quad_perm [1, 0, 3, 2]
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+}
+
 // ============================================================================
 // backward dK/dV: WG = 4 waves x 32 keys = 128 keys; loop over 64-query tiles
 //   S = Q.K^T, dP = dO.V^T (keys on lanes, queries in registers)
 //   dV^T += dO^T.(P o Z),  dK^T += Q^T.dS
+// The Q / dO tiles and their lse / delta row constants are double-buffered:
+// tile i+1 streams into the second LDS buffer (global_load_lds) while tile i
+// computes, one vmcnt drain + barrier per tile.
+// Dropout: lanes 2j, 2j+1 hold keys 2j, 2j+1 = the two 16-bit halves of ONE
+// hash per query row, so each lane hashes every other query row and the
+// pair trades results through DPP (one hash per two elements, as fwd / dQ).
 // ============================================================================
 template <int D, bool CAUSAL, bool DROP, bool KB>
 __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int QT = 64, TB = QT * D * 2;
-  // layout: [Q tile][dO tile][lse2 64 floats][delta 64 floats]
-  char* qt = smem;
-  char* gt = smem + TB;
-  float* lse_s = reinterpret_cast<float*>(smem + 2 * TB);
-  float* dl_s = lse_s + QT;
+  // one buffer: [Q tile][dO tile][lse2 64 floats][delta 64 floats]
+  constexpr int BUF = 2 * TB + 2 * QT * 4;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
   const int nk = (P.Sk + 127) / 128;
   const int nblk = nk * P.B * P.H;
@@ -503,62 +570,111 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnParams P) {
   const uint32_t cb = DROP ? (lowbias32((uint32_t)bh ^ P.khi) ^ P.klo) : 0u;
 
   const int q_begin = CAUSAL ? (kblock * 128 / QT) * QT : 0;
-  for (int qb = q_begin; qb < P.Sq; qb += QT) {
-    __syncthreads();  // previous tile fully consumed
-    Glds<D, QT>::load(qp, P.sq_s, qb, P.Sq, qt, w, lane);
-    Glds<D, QT>::load(dop, P.so_s, qb, P.Sq, gt, w, lane);
+  const int ntiles = P.Sq > q_begin ? (P.Sq - q_begin + QT - 1) / QT : 0;
+  // row constants of tile qb: loaded BEFORE the tile's DMA is issued (vmcnt
+  // retires in order), written to LDS after the compute of the current tile
+  float nl = INFINITY, nd = 0.f;
+  auto rowconst_load = [&](int qb) {
     if (tid < QT) {
       const int q = qb + tid;
-      lse_s[tid] = q < P.Sq ? P.lse[(long)bh * P.Sq + q] * LOG2E : INFINITY;
-      dl_s[tid] = q < P.Sq ? P.delta[(long)bh * P.Sq + q] : 0.f;
+      nl = q < P.Sq ? P.lse[(long)bh * P.Sq + q] * LOG2E : INFINITY;
+      nd = q < P.Sq ? P.delta[(long)bh * P.Sq + q] : 0.f;
     }
+  };
+  auto rowconst_store = [&](char* buf) {
+    if (tid < QT) {
+      float* c = reinterpret_cast<float*>(buf + 2 * TB);
+      c[tid] = nl;
+      c[QT + tid] = nd;
+    }
+  };
+  GldsStream<D, QT> qld, gld;
+  qld.init(qp, P.sq_s, P.Sq, w, lane);
+  gld.init(dop, P.so_s, P.Sq, w, lane);
+  if (ntiles > 0) {
+    rowconst_load(q_begin);
+    qld.load(q_begin, smem, lane);
+    gld.load(q_begin, smem + TB, lane);
+    rowconst_store(smem);
+  }
+  glds_wait();
+  __syncthreads();
+
+  for (int it = 0; it < ntiles; ++it) {
+    const int qb = q_begin + it * QT;
+    const char* cur = smem + (it & 1) * BUF;
+    char* nxt = smem + ((it & 1) ^ 1) * BUF;
+    const bool more = it + 1 < ntiles;
+    if (more) {
+      rowconst_load(qb + QT);
+      qld.load(qb + QT, nxt, lane);
+      gld.load(qb + QT, nxt + TB, lane);
+    }
+    const char* qt = cur;
+    const char* gt = cur + TB;
+    const float* lse_s = reinterpret_cast<const float*>(cur + 2 * TB);
+    const float* dl_s = lse_s + QT;
+    if (!(CAUSAL && qb + QT - 1 < wk0)) {  // else: whole tile above this wave's keys
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int q0 = qb + 32 * t;
+        if (CAUSAL && q0 + 31 < wk0) continue;
+        floatx16 sacc, dpacc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[i] = dpacc[i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s) {
+          sacc = mfma(row_frag<D>(qt, 32 * t + (lane & 31), s, h), kf[s], sacc);
+          dpacc = mfma(row_frag<D>(gt, 32 * t + (lane & 31), s, h), vf[s], dpacc);
+        }
+        float zs[16];
+        if (DROP) {
+          // registers i, i+1 (i even) are query rows q, q+1 of this lane's key
+#pragma unroll
+          for (int i = 0; i < 16; i += 2) {
+            const int q = qb + 32 * t + crow(i, h);
+            const uint32_t mine =
+                lowbias32((((uint32_t)(q + (lane & 1))) << 16 | ((uint32_t)ki >> 1)) ^ cb);
+            const uint32_t other = dpp_swap1(mine);
+            const uint32_t hq = (lane & 1) ? other : mine;   // hash of row q
+            const uint32_t hq1 = (lane & 1) ? mine : other;  // hash of row q + 1
+            const uint32_t r0 = (lane & 1) ? (hq >> 16) : (hq & 0xffffu);
+            const uint32_t r1 = (lane & 1) ? (hq1 >> 16) : (hq1 & 0xffffu);
+            zs[i] = r0 >= P.thr ? P.drop_scale : 0.f;
+            zs[i + 1] = r1 >= P.thr ? P.drop_scale : 0.f;
+          }
+        }
+        floatx16 pd;  // dropped probabilities (for dV)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int ql_ = 32 * t + crow(i, h);
+          const int q = qb + ql_;
+          float p = fexp2(sacc[i] * sl2 + kb2 - lse_s[ql_]);
+          if ((CAUSAL && ki > q) || !kvalid || q >= P.Sq) p = 0.f;
+          const float z = DROP ? zs[i] : 1.f;
+          pd[i] = p * z;
+          sacc[i] = p * (dpacc[i] * z - dl_s[ql_]);  // dS
+        }
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          bf16x8 pf, df;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            pf[j] = (__bf16)pd[8 * ss + j];
+            df[j] = (__bf16)sacc[8 * ss + j];
+          }
+          const int qbase = 32 * t + 16 * ss + 4 * h;
+#pragma unroll
+          for (int dt = 0; dt < D / 32; ++dt) {
+            dvacc[dt] = mfma(tr_frag<D>(gt, qbase, dt, lane), pf, dvacc[dt]);
+            dkacc[dt] = mfma(tr_frag<D>(qt, qbase, dt, lane), df, dkacc[dt]);
+          }
+        }
+      }
+    }
+    if (more) rowconst_store(nxt);
     glds_wait();
     __syncthreads();
-    if (CAUSAL && qb + QT - 1 < wk0) continue;  // whole tile above this wave's keys
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int q0 = qb + 32 * t;
-      if (CAUSAL && q0 + 31 < wk0) continue;
-      floatx16 sacc, dpacc;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sacc[i] = dpacc[i] = 0.f;
-#pragma unroll
-      for (int s = 0; s < D / 16; ++s) {
-        sacc = mfma(row_frag<D>(qt, 32 * t + (lane & 31), s, h), kf[s], sacc);
-        dpacc = mfma(row_frag<D>(gt, 32 * t + (lane & 31), s, h), vf[s], dpacc);
-      }
-      floatx16 pd;  // dropped probabilities (for dV)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int ql_ = 32 * t + crow(i, h);
-        const int q = qb + ql_;
-        float p = exp2f(sacc[i] * sl2 + kb2 - lse_s[ql_]);
-        if ((CAUSAL && ki > q) || !kvalid || q >= P.Sq) p = 0.f;
-        float z = 1.f;
-        if (DROP) {
-          const uint32_t hh = lowbias32((((uint32_t)q) << 16 | ((uint32_t)ki >> 1)) ^ cb);
-          const uint32_t r = (ki & 1) ? (hh >> 16) : (hh & 0xffffu);
-          z = r >= P.thr ? P.drop_scale : 0.f;
-        }
-        pd[i] = p * z;
-        sacc[i] = p * (dpacc[i] * z - dl_s[ql_]);  // dS
-      }
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        bf16x8 pf, df;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          pf[j] = (__bf16)pd[8 * ss + j];
-          df[j] = (__bf16)sacc[8 * ss + j];
-        }
-        const int qbase = 32 * t + 16 * ss + 4 * h;
-#pragma unroll
-        for (int dt = 0; dt < D / 32; ++dt) {
-          dvacc[dt] = mfma(tr_frag<D>(gt, qbase, dt, lane), pf, dvacc[dt]);
-          dkacc[dt] = mfma(tr_frag<D>(qt, qbase, dt, lane), df, dkacc[dt]);
-        }
-      }
-    }
   }
   if (ki < P.Sk) {
     uint16_t* dkp = P.dk + b * P.sdk_b + hd * P.sdk_h + (long)ki * P.sdk_s;
@@ -603,17 +719,27 @@ AttnParams make_params(const void* q, const void* k, const void* v, const long* 
 
 }  // namespace
 
+// Launch with dynamic LDS; above 64 KiB the kernel must opt in (up to the
+// 160 KiB of a CU).
+static void fa_launch(void (*kernel)(AttnParams), int grid, size_t smem, hipStream_t st,
+                      const AttnParams& P) {
+  if (smem > 65536)
+    (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)smem);
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(256), smem, st, P);
+}
+
 #define FA_DISPATCH_D(KERNEL, DD, causal, drop, kbias, grid, smem, st, P)         \
   do {                                                                          \
     if (causal) {                                                               \
-      if (drop) KERNEL<DD, true, true, false><<<grid, 256, smem, st>>>(P);      \
-      else KERNEL<DD, true, false, false><<<grid, 256, smem, st>>>(P);          \
+      if (drop) fa_launch(KERNEL<DD, true, true, false>, grid, smem, st, P);    \
+      else fa_launch(KERNEL<DD, true, false, false>, grid, smem, st, P);        \
     } else if (kbias) {                                                         \
-      if (drop) KERNEL<DD, false, true, true><<<grid, 256, smem, st>>>(P);      \
-      else KERNEL<DD, false, false, true><<<grid, 256, smem, st>>>(P);          \
+      if (drop) fa_launch(KERNEL<DD, false, true, true>, grid, smem, st, P);    \
+      else fa_launch(KERNEL<DD, false, false, true>, grid, smem, st, P);        \
     } else {                                                                    \
-      if (drop) KERNEL<DD, false, true, false><<<grid, 256, smem, st>>>(P);     \
-      else KERNEL<DD, false, false, false><<<grid, 256, smem, st>>>(P);         \
+      if (drop) fa_launch(KERNEL<DD, false, true, false>, grid, smem, st, P);   \
+      else fa_launch(KERNEL<DD, false, false, false>, grid, smem, st, P);       \
     }                                                                           \
   } while (0)
 // key bias is only instantiated for non-causal attention (BERT-style padding
@@ -686,7 +812,7 @@ extern "C" int fx_flash_bwd(const void* q, const void* k, const void* v, const v
   }
   {
     const int nk = (Sk + 127) / 128;
-    const size_t smem = 2 * 64 * D * 2 + 2 * 64 * 4;
+    const size_t smem = 2 * (2 * 64 * D * 2 + 2 * 64 * 4);  // double-buffered Q/dO tiles
     FA_DISPATCH(fa_bwd_dkdv_kernel, D, causal, p > 0.f, kbias != nullptr, nk * B * H, smem, st,
                 P);
   }

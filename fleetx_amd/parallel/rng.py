@@ -112,7 +112,9 @@ class RNGStream:
         self.offset = 0
 
     def next_key(self):
-        k = splitmix64(self.seed ^ splitmix64(self.offset))
+        # 63-bit keys: they travel as int64 scalars through autograd (and the
+        # profiler's record_shapes), which rejects values >= 2^63
+        k = splitmix64(self.seed ^ splitmix64(self.offset)) & 0x7FFFFFFFFFFFFFFF
         self.offset += 1
         return k
 
