@@ -34,6 +34,10 @@ MODELS = {
     "gpt-tiny": (256, 2, 4),
 }
 PEAK_BF16 = 2.5e15  # MI355X dense bf16 (spec), per GPU
+# Reference (V100) throughput per GPU on the same model/batch/seq:
+# row 1 (345M single card, 16.2k tokens/s) and row 4 (1.3B dp8, ~3.3k tokens/s/GPU,
+# derived).  The 6.7B headline config has no published reference number.
+REF_TOKENS_PER_GPU = {"gpt-345M": 16200.0, "gpt3-1.3B": 3300.0}
 
 
 
@@ -165,7 +169,9 @@ def main():
             if args.model == "gpt3-6.7B" else "tokens/sec %s" % args.model,
             "value": round(tps, 1), "unit": "tokens/s", "n_gpus": n, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": round(tps / (REF_TOKENS_PER_GPU[args.model] * n), 3)
+            if args.model in REF_TOKENS_PER_GPU else None,
             "dtype": "bf16" if engine._dtype == torch.bfloat16 else str(engine._dtype).replace("torch.", ""), "data": "synthetic (random tokens), random-init weights",
             "config": {"model": args.model, "global_batch": global_batch, "seq_len": S,
                        "parallelism": par, "micro_batch": micro,
