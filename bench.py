@@ -172,7 +172,9 @@ def main():
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(tps / (REF_TOKENS_PER_GPU[args.model] * n), 3)
             if args.model in REF_TOKENS_PER_GPU else None,
-            "dtype": "bf16" if engine._dtype == torch.bfloat16 else str(engine._dtype).replace("torch.", ""), "data": "synthetic (random tokens), random-init weights",
+            "dtype": "bf16" if engine._dtype == torch.bfloat16
+            else str(engine._dtype).replace("torch.", ""),
+            "data": "synthetic (random tokens), random-init weights",
             "config": {"model": args.model, "global_batch": global_batch, "seq_len": S,
                        "parallelism": par, "micro_batch": micro,
                        "dropout": drop, "recompute": recompute},

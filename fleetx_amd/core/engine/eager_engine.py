@@ -119,6 +119,7 @@ class EagerEngine(BasicEngine):
         self._output_dir = sl.get("output_dir", "./output")
         self._ckpt_dir = sl.get("ckpt_dir")
         self._nan_guard = e.get("nan_guard", "off")
+        self._metrics_file = e.get("metrics_file") or os.environ.get("FLEETX_METRICS_FILE")
         self._fault = os.environ.get("FLEETX_FAULT_INJECT")  # "rank:step" -> os._exit(17)
 
         self.hcg = topo.get_hcg()
@@ -285,6 +286,7 @@ class EagerEngine(BasicEngine):
                 self._module.training_step_end({"epoch": epoch, "batch": global_step, "loss": lval,
                                                 "train_cost": cost, "lr": self._current_lr(),
                                                 "total_batch": total})
+                self._write_metrics(epoch, global_step, lval, cost)
                 loss_acc, n_acc = None, 0
                 t0 = time.time()
             if self._run_mode == "step" and valid_loader is not None and \
@@ -298,6 +300,28 @@ class EagerEngine(BasicEngine):
             if self._run_mode == "step" and global_step >= self._max_steps:
                 return global_step, True
         return global_step, False
+
+    def _write_metrics(self, epoch, step, loss, step_time):
+        """Optional JSONL metrics sink (``Engine.metrics_file``):
+        one record per logging window from global rank 0 (the loss is already
+        broadcast from the last pipeline stage)."""
+        if not self._metrics_file or env.get_rank() != 0:
+            return
+        import json
+        rec = {"time": round(time.time(), 3), "epoch": epoch, "step": step, "loss": loss,
+               "lr": self._current_lr(), "step_time_s": round(step_time, 6),
+               "consumed_samples": self.consumed_samples}
+        if self.optimizer is not None and getattr(self.optimizer, "last_grad_norm", None) is not None:
+            rec["grad_norm"] = float(self.optimizer.last_grad_norm)
+        tokens = getattr(self._module, "tokens_per_step", None)
+        if callable(tokens):
+            rec["tokens_per_s"] = round(tokens() / max(step_time, 1e-9), 1)
+        if torch.cuda.is_available():
+            rec["max_mem_gb"] = round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)
+        d = os.path.dirname(os.path.abspath(self._metrics_file))
+        os.makedirs(d, exist_ok=True)
+        with open(self._metrics_file, "a") as f:
+            f.write(json.dumps(rec) + "\n")
 
     def _reduce_log_loss(self, loss_acc, n):
         """Loss for the log line: mean over the window; under PP it lives on

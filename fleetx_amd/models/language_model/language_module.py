@@ -56,6 +56,10 @@ class LanguageModule(BasicModule):
             % (log_dict["epoch"], log_dict["batch"], log_dict["loss"], log_dict["train_cost"], speed,
                speed * tokens, speed * tokens / self.data_world_size, log_dict["lr"]))
 
+    def tokens_per_step(self):
+        """Tokens of one optimizer step over the whole job (the ips_total numerator)."""
+        return self.configs.Global.global_batch_size * self._seq_len()
+
     def _seq_len(self):
         try:
             return self.configs.Data.Train.dataset.max_seq_len

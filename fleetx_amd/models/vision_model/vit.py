@@ -192,20 +192,37 @@ class ViT(nn.Module):
         self.load_state_dict(sd, strict=False)
 
 
+_QKV = dict(qkv_bias=True, epsilon=1e-6)
 PRESETS = {
-    "ViT_base_patch16_224": dict(img_size=224, patch_size=16, embed_dim=768, depth=12, num_heads=12, mlp_ratio=4, qkv_bias=True, epsilon=1e-6),
-    "ViT_base_patch16_384": dict(img_size=384, patch_size=16, embed_dim=768, depth=12, num_heads=12, mlp_ratio=4, qkv_bias=True, epsilon=1e-6),
-    "ViT_base_patch32_224": dict(img_size=224, patch_size=32, embed_dim=768, depth=12, num_heads=12, mlp_ratio=4, qkv_bias=True, epsilon=1e-6),
-    "ViT_base_patch32_384": dict(img_size=384, patch_size=32, embed_dim=768, depth=12, num_heads=12, mlp_ratio=4, qkv_bias=True, epsilon=1e-6),
-    "ViT_large_patch16_224": dict(img_size=224, patch_size=16, embed_dim=1024, depth=24, num_heads=16, mlp_ratio=4, qkv_bias=True, epsilon=1e-6),
-    "ViT_large_patch16_384": dict(img_size=384, patch_size=16, embed_dim=1024, depth=24, num_heads=16, mlp_ratio=4, qkv_bias=True, epsilon=1e-6),
-    "ViT_large_patch32_224": dict(img_size=224, patch_size=32, embed_dim=1024, depth=24, num_heads=16, mlp_ratio=4, qkv_bias=True, epsilon=1e-6),
-    "ViT_large_patch32_384": dict(img_size=384, patch_size=32, embed_dim=1024, depth=24, num_heads=16, mlp_ratio=4, qkv_bias=True, epsilon=1e-6),
-    "ViT_huge_patch14_224": dict(img_size=224, patch_size=14, embed_dim=1280, depth=32, num_heads=16, mlp_ratio=4, representation_size=None),
-    "ViT_huge_patch14_384": dict(img_size=384, patch_size=14, embed_dim=1280, depth=32, num_heads=16, mlp_ratio=4, representation_size=None),
-    "ViT_g_patch14_224": dict(img_size=224, patch_size=14, embed_dim=1408, depth=40, num_heads=16, mlp_ratio=4.364, qkv_bias=True, epsilon=1e-6, representation_size=1408),
-    "ViT_G_patch14_224": dict(img_size=224, patch_size=14, embed_dim=1664, depth=48, num_heads=16, mlp_ratio=4.9231, qkv_bias=True, epsilon=1e-6, representation_size=1664),
-    "ViT_6B_patch14_224": dict(img_size=224, patch_size=14, embed_dim=2320, depth=80, num_heads=16, mlp_ratio=4.955, qkv_bias=True, epsilon=1e-6, representation_size=2320),
+    "ViT_base_patch16_224": dict(
+        img_size=224, patch_size=16, embed_dim=768, depth=12, num_heads=12, mlp_ratio=4, **_QKV),
+    "ViT_base_patch16_384": dict(
+        img_size=384, patch_size=16, embed_dim=768, depth=12, num_heads=12, mlp_ratio=4, **_QKV),
+    "ViT_base_patch32_224": dict(
+        img_size=224, patch_size=32, embed_dim=768, depth=12, num_heads=12, mlp_ratio=4, **_QKV),
+    "ViT_base_patch32_384": dict(
+        img_size=384, patch_size=32, embed_dim=768, depth=12, num_heads=12, mlp_ratio=4, **_QKV),
+    "ViT_large_patch16_224": dict(
+        img_size=224, patch_size=16, embed_dim=1024, depth=24, num_heads=16, mlp_ratio=4, **_QKV),
+    "ViT_large_patch16_384": dict(
+        img_size=384, patch_size=16, embed_dim=1024, depth=24, num_heads=16, mlp_ratio=4, **_QKV),
+    "ViT_large_patch32_224": dict(
+        img_size=224, patch_size=32, embed_dim=1024, depth=24, num_heads=16, mlp_ratio=4, **_QKV),
+    "ViT_large_patch32_384": dict(
+        img_size=384, patch_size=32, embed_dim=1024, depth=24, num_heads=16, mlp_ratio=4, **_QKV),
+    "ViT_huge_patch14_224": dict(
+        img_size=224, patch_size=14, embed_dim=1280, depth=32, num_heads=16, mlp_ratio=4, representation_size=None),
+    "ViT_huge_patch14_384": dict(
+        img_size=384, patch_size=14, embed_dim=1280, depth=32, num_heads=16, mlp_ratio=4, representation_size=None),
+    "ViT_g_patch14_224": dict(
+        img_size=224, patch_size=14, embed_dim=1408, depth=40, num_heads=16, mlp_ratio=4.364,
+        representation_size=1408, **_QKV),
+    "ViT_G_patch14_224": dict(
+        img_size=224, patch_size=14, embed_dim=1664, depth=48, num_heads=16, mlp_ratio=4.9231,
+        representation_size=1664, **_QKV),
+    "ViT_6B_patch14_224": dict(
+        img_size=224, patch_size=14, embed_dim=2320, depth=80, num_heads=16, mlp_ratio=4.955,
+        representation_size=2320, **_QKV),
 }
 
 

@@ -28,7 +28,15 @@ def get_world_size():
 def init_dist_env(config, backend=None):
     """Create the process group and the hybrid topology from ``Distributed``."""
     d = config.Distributed
-    topo.init_distributed(backend=backend)
+    # collective debugging (SURVEY §5.2, new vs. the reference): "detail" wraps every
+    # process group so each collective first cross-checks op / shape / dtype
+    # fingerprints across ranks and reports the mismatching rank instead of hanging.
+    dbg = str(d.get("debug", os.environ.get("FLEETX_COLLECTIVE_CHECK", "off")) or "off").lower()
+    if dbg in ("1", "detail", "on", "true"):
+        os.environ.setdefault("TORCH_DISTRIBUTED_DEBUG", "DETAIL")
+    elif dbg == "info":
+        os.environ.setdefault("TORCH_DISTRIBUTED_DEBUG", "INFO")
+    topo.init_distributed(backend=backend, timeout_s=int(d.get("timeout_s", 1800) or 1800))
     hcg = topo.init_hcg(dp=d.dp_degree, mp=d.mp_degree, pp=d.pp_degree,
                         sharding=d.sharding.sharding_degree)
     return hcg

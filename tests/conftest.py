@@ -1,3 +1,4 @@
+"""pytest setup: the ``gpu`` marker and the repo root on sys.path."""
 import os
 import sys
 

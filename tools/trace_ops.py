@@ -56,7 +56,8 @@ def main():
     for e in prof.events():
         if e.name == "aten::copy_" and e.device_type.name == "CPU":
             par = e.cpu_parent.name if e.cpu_parent is not None else "-"
-            gp = e.cpu_parent.cpu_parent.name if e.cpu_parent is not None and e.cpu_parent.cpu_parent is not None else "-"
+            gpar = e.cpu_parent.cpu_parent if e.cpu_parent is not None else None
+            gp = gpar.name if gpar is not None else "-"
             print("COPY", e.input_shapes, "<-", par, "<-", gp)
     # which CPU ops issued device memcpys
     for e in prof.events():
