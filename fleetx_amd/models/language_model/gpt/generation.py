@@ -169,6 +169,45 @@ def _layer_decode(layer, x, cache, li, pos, lens_after):
     return ops.bias_dropout_add(m, mb, x2)
 
 
+class _GraphedDecodeStep:
+    """The per-token decode step (embedding -> L decoder layers against the KV
+    cache -> final LN -> logits) captured once into a HIP graph and replayed
+    for every following token.
+
+    At decode batch sizes every op is a tiny, launch-bound kernel (~10 per
+    layer), so the eager loop is host-bound; a replay issues the whole step as
+    one graph launch.  This is the MI355X counterpart of the reference's
+    static inference program with ``fused_multi_transformer`` (K19 / N-12):
+    the same fused HIP kernels, with the launch overhead removed by the graph
+    instead of a tracing compiler.  The first call runs eagerly (it is also
+    that token's real work) and captures; inputs live in static tensors.
+    """
+
+    def __init__(self, gen, cache, batch):
+        self.gen, self.cache = gen, cache
+        dev = cache.k[0].device
+        self.nxt = torch.zeros(batch, dtype=torch.long, device=dev)
+        self.cur = torch.zeros(batch, dtype=torch.long, device=dev)
+        self.graph = None
+        self.logits = None
+
+    def __call__(self, nxt, cur):
+        self.nxt.copy_(nxt)
+        self.cur.copy_(cur)
+        if self.graph is None:
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):  # warm-up off the capture stream
+                out = self.gen._decode_step(self.nxt, self.cur, self.cache)
+            torch.cuda.current_stream().wait_stream(side)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.logits = self.gen._decode_step(self.nxt, self.cur, self.cache)
+            return out
+        self.graph.replay()
+        return self.logits
+
+
 class GPTForGeneration(torch.nn.Module):
     def __init__(self, pretrain_model, configs):
         super().__init__()
@@ -191,6 +230,7 @@ class GPTForGeneration(torch.nn.Module):
         self.forced_bos_token_id = c.get("forced_bos_token_id")
         self.forced_eos_token_id = c.get("forced_eos_token_id")
         self.num_return_sequences = c.get("num_return_sequences", 1)
+        self.use_hip_graph = bool(c.get("use_hip_graph", True))
         if self.decode_strategy not in ("sampling", "greedy_search"):
             raise ValueError("decode_strategy must be sampling or greedy_search")
 
@@ -208,6 +248,18 @@ class GPTForGeneration(torch.nn.Module):
         if self.forced_eos_token_id is not None:
             procs.append(ForcedEOSTokenLogitsProcessor(max_len, self.forced_eos_token_id))
         return procs
+
+    def _decode_step(self, nxt, cur, cache):
+        """Embed token ``nxt`` at position ``cur`` [B], run every layer against
+        the KV cache (appending this token), return fp32 logits [B, V]."""
+        x = ops.embedding(nxt[:, None], self.gpt.embeddings.word_embeddings.weight,
+                          cur[:, None], self.gpt.embeddings.position_embeddings, 0) \
+            if topo.mp_world_size() == 1 else self.gpt.embeddings(nxt[:, None], cur[:, None])
+        after = (cur + 1).to(torch.int32)
+        for li, layer in enumerate(self.gpt.layers):
+            x = _layer_decode(layer, x, cache, li, cur, after)
+        x = self.gpt.final_ln(x)
+        return self._logits(x[:, 0])
 
     def _logits(self, h):
         w = self.gpt.embeddings.word_embeddings.weight
@@ -255,6 +307,7 @@ class GPTForGeneration(torch.nn.Module):
         out_tokens = []
         cur = lens.clone()
         history = input_ids.clone()
+        graphed = None
         for step in range(max_new):
             if cur.max().item() >= total:
                 break
@@ -282,15 +335,12 @@ class GPTForGeneration(torch.nn.Module):
                 unfinished = unfinished & (nxt != eos)
                 if not bool(unfinished.any()):
                     break
-            # ---- one decode step
-            x = ops.embedding(nxt[:, None], self.gpt.embeddings.word_embeddings.weight,
-                              cur[:, None], self.gpt.embeddings.position_embeddings, 0) \
-                if topo.mp_world_size() == 1 else self.gpt.embeddings(nxt[:, None], cur[:, None])
-            after = (cur + 1).to(torch.int32)
-            for li, layer in enumerate(self.gpt.layers):
-                x = _layer_decode(layer, x, cache, li, cur, after)
-            x = self.gpt.final_ln(x)
-            logits = self._logits(x[:, 0])
+            # ---- one decode step (replayed from a HIP graph after the first token)
+            if graphed is None and self.use_hip_graph and dev.type == "cuda" \
+                    and topo.mp_world_size() == 1:
+                graphed = _GraphedDecodeStep(self, cache, B)
+            logits = graphed(nxt, cur) if graphed is not None else \
+                self._decode_step(nxt, cur, cache)
             cur = cur + 1
         if not out_tokens:
             return torch.zeros(B, 0, dtype=torch.long, device=dev), scores

@@ -122,7 +122,8 @@ def test_train_cli_cpu_fp32(tmp_path):
            "-o", "Data.Eval.dataset.vocab_size=512", "-o", "Global.local_batch_size=2",
            "-o", "Global.micro_batch_size=2", "-o", "Data.Train.loader.num_workers=0",
            "-o", "Data.Eval.loader.num_workers=0",
-           "-o", "Engine.save_load.output_dir=%s" % tmp_path, "-o", "Engine.save_load.save_steps=2"]
+           "-o", "Engine.save_load.output_dir=%s" % tmp_path, "-o", "Engine.save_load.save_steps=2",
+           "-o", "Engine.metrics_file=%s" % (tmp_path / "metrics.jsonl")]
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
@@ -131,3 +132,7 @@ def test_train_cli_cpu_fp32(tmp_path):
     loss0 = float(lines[0].split("loss: ")[1].split(",")[0])
     assert abs(loss0 - math.log(512)) < 0.3
     assert (tmp_path / "epoch_0_step_2" / "model.pdparams").exists()
+    import json
+    recs = [json.loads(l) for l in open(tmp_path / "metrics.jsonl")]
+    assert [r["step"] for r in recs] == [1, 2, 3, 4]
+    assert all(r["tokens_per_s"] > 0 and "grad_norm" in r and "lr" in r for r in recs)
