@@ -481,8 +481,16 @@ class EagerEngine(BasicEngine):
     # ------------------------------------------------------------------ export / inference
     def export(self):
         from ...utils.export import export_inference_model
-        out = os.path.join(self._output_dir, "rank_{}".format(self._dp_rank))
-        export_inference_model(self._module, out)
+        # one directory per tensor-parallel shard (rank_{mp_rank}); data-parallel
+        # replicas hold identical weights, so only the first replica writes
+        if self.hcg.mp_degree > 1:
+            if self._dp_rank != 0 or self._sharding_rank != 0:
+                return
+            out = os.path.join(self._output_dir, "rank_{}".format(self._mp_rank))
+        else:
+            out = os.path.join(self._output_dir, "rank_{}".format(self._dp_rank))
+        with self._params_gathered():
+            export_inference_model(self._module, out, mp_degree=self.hcg.mp_degree)
         logger.info("export model to %s" % out)
 
     def inference(self, data):

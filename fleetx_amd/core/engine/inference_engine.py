@@ -24,14 +24,29 @@ from ...utils.log import logger
 class InferenceEngine:
     def __init__(self, model_dir, mp_degree=1, use_graph=True, dtype=None):
         self.model_dir = model_dir
-        self.mp_degree = mp_degree
-        rank = int(os.environ.get("RANK", "0"))
-        d = os.path.join(model_dir, "rank_{}".format(rank % max(1, mp_degree)))
+        self.mp_degree = max(1, int(mp_degree or 1))
+        if self.mp_degree > 1:
+            # reference: one predictor per rank over an mp comm ring (inference_engine.py:89-124);
+            # here every rank joins an RCCL (gloo on CPU) group and runs its TP shard
+            from ...parallel import topology as topo
+            ws = int(os.environ.get("WORLD_SIZE", "1"))
+            if ws != self.mp_degree:
+                raise ValueError("mp_degree={} inference needs WORLD_SIZE={} (got {}); launch one "
+                                 "process per shard".format(self.mp_degree, self.mp_degree, ws))
+            topo.init_distributed()
+            self.hcg = topo.init_hcg(mp=self.mp_degree)
+            rank = self.hcg.mp_rank
+        else:
+            rank = int(os.environ.get("RANK", "0"))
+        d = os.path.join(model_dir, "rank_{}".format(rank % self.mp_degree))
         if not os.path.isdir(d):
             d = os.path.join(model_dir, "rank_0") if os.path.isdir(
                 os.path.join(model_dir, "rank_0")) else model_dir
         self._check_model(d)
         self.meta, sd = load_exported(d)
+        if int(self.meta.get("mp_degree", 1)) != self.mp_degree:
+            raise ValueError("{} was exported with mp_degree={}, engine asked for {}".format(
+                d, self.meta.get("mp_degree", 1), self.mp_degree))
         self.device = torch.device("cuda", torch.cuda.current_device()) \
             if torch.cuda.is_available() else torch.device("cpu")
         self.dtype = dtype or (torch.bfloat16 if self.device.type == "cuda" else torch.float32)
@@ -57,15 +72,16 @@ class InferenceEngine:
             "Model": dict(meta["Model"], module=meta["module"]),
             "Generation": meta.get("Generation", {}),
             "Engine": {"max_steps": 1, "mix_precision": {"use_pure_fp16": False}},
-            "Distributed": {"dp_degree": 1, "mp_degree": 1, "pp_degree": 1,
+            "Distributed": {"dp_degree": 1, "mp_degree": self.mp_degree, "pp_degree": 1,
                             "sharding": {"sharding_degree": 1}},
             "Optimizer": {"name": "FusedAdamW"},
         })
+        cfg.Model["sequence_parallel"] = False
         cfg.Global.setdefault("local_batch_size", 1)
         cfg.Global["global_batch_size"] = None
         cfg.Global["micro_batch_size"] = 1
         _fill_defaults(cfg)
-        process_dist_config(cfg.Distributed, 1)
+        process_dist_config(cfg.Distributed, self.mp_degree)
         process_global_configs(cfg)
         cfg.Engine["accumulate_steps"] = 1
         cfg.Engine["test_iters"] = 1
@@ -108,7 +124,7 @@ class InferenceEngine:
             lens = inputs[1] if len(inputs) > 1 else None
             out, scores = model.generate(inputs[0], lens)
             return [out.cpu().numpy(), scores.float().cpu().numpy()]
-        if self.use_graph:
+        if self.use_graph and self.mp_degree == 1:
             try:
                 out = self._graph_forward(inputs)
             except RuntimeError as e:  # capture unsupported for this graph: run eagerly
@@ -117,5 +133,8 @@ class InferenceEngine:
                 out = model(*inputs)
         else:
             out = model(*inputs)
+        if self.mp_degree > 1 and torch.is_tensor(out):
+            from ...parallel import mappings as M
+            out = M.gather_from_mp(out)  # vocab-parallel logits -> full vocabulary
         outs = out if isinstance(out, (tuple, list)) else [out]
         return [o.float().cpu().numpy() for o in outs]

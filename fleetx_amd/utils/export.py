@@ -32,7 +32,9 @@ def _plain(obj):
     return str(obj)
 
 
-def export_inference_model(module, output_dir):
+def export_inference_model(module, output_dir, mp_degree=1):
+    """``mp_degree > 1``: ``output_dir`` is this tensor-parallel rank's
+    ``rank_{mp_rank}`` directory and the weights are its shard."""
     os.makedirs(output_dir, exist_ok=True)
     cfg = module.configs
     try:
@@ -45,11 +47,12 @@ def export_inference_model(module, output_dir):
         "Generation": _plain(dict(cfg.get("Generation", {}) or {})),
         "Global": _plain(dict(cfg.Global)),
         "input_spec": [[n, s, str(d).replace("torch.", "")] for n, s, d in spec],
+        "mp_degree": int(mp_degree),
         "format": "fleetx-amd-export-v1",
     }
     with open(os.path.join(output_dir, "model.json"), "w") as f:
         json.dump(meta, f, indent=2)
-    sd = {k: v.detach().cpu() for k, v in module.model.state_dict().items()}
+    sd = {k: v.detach().to("cpu", copy=True) for k, v in module.model.state_dict().items()}
     torch.save(sd, os.path.join(output_dir, "model.pdparams"))
     return output_dir
 
