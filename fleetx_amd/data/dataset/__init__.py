@@ -1,9 +1,11 @@
 """Dataset registry."""
 from .gpt_dataset import (GPTDataset, SyntheticGPTDataset, LM_Eval_Dataset,  # noqa: F401
                           Lambada_Eval_Dataset)
+from .ernie_dataset import ErnieDataset  # noqa: F401
 
 DATASETS = {
     "GPTDataset": GPTDataset,
+    "ErnieDataset": ErnieDataset,
     "SyntheticGPTDataset": SyntheticGPTDataset,
     "LM_Eval_Dataset": LM_Eval_Dataset,
     "Lambada_Eval_Dataset": Lambada_Eval_Dataset,

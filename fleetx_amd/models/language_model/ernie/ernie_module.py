@@ -37,10 +37,22 @@ class ErnieModule(BasicModule):
         self.nranks = env.get_world_size()
         self.data_world_size = env.get_data_world_size()
         super().__init__(configs)
-        self.criterion = ErniePretrainingCriterion(with_nsp_loss=False)
+        # sentence-pair samples (ErnieDataset) train MLM + next-sentence prediction
+        try:
+            ds_name = self.configs.Data.Train.dataset.name
+        except (AttributeError, KeyError):
+            ds_name = None
+        self.pair_data = ds_name == "ErnieDataset"
+        self.criterion = ErniePretrainingCriterion(with_nsp_loss=self.pair_data)
         m = self.configs.Model
         self.mask_token_id = m.get("mask_token_id", m.vocab_size - 1)
         self.mask_prob = m.get("masked_lm_prob", 0.15)
+        ds = {}
+        try:
+            ds = dict(self.configs.Data.Train.dataset)
+        except (AttributeError, KeyError):
+            pass
+        self.special_ids = tuple({m.get("pad_token_id", 0), ds.get("cls_id", 1), ds.get("sep_id", 2)})
 
     def process_configs(self, configs):
         process_data_configs(configs)
@@ -65,10 +77,15 @@ class ErnieModule(BasicModule):
         tokens = batch[0]
         vocab = self.configs.Model.vocab_size
         pad = self.configs.Model.get("pad_token_id", 0)
+        special = self.special_ids if self.pair_data else (pad,)
         inputs, labels = mlm_mask(tokens, vocab, self.mask_token_id, self.mask_prob,
-                                  special_ids=(pad,))
+                                  special_ids=special)
         flat = labels.reshape(-1)
         pos = torch.nonzero(flat >= 0).reshape(-1)
+        if self.pair_data:  # (tokens, token_type_ids, next_sentence_label, length)
+            scores, rel = self.model(inputs, token_type_ids=batch[1], masked_positions=pos)
+            mlm, nsp = self.criterion(scores, rel, flat[pos], batch[2])
+            return mlm + nsp
         scores, rel = self.model(inputs, masked_positions=pos)
         return self.criterion(scores, rel, flat[pos])
 

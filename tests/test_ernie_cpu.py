@@ -3,6 +3,8 @@ TransformerEncoderLayer, padding-mask semantics, heads, dynamic MLM masking
 and an end-to-end pretraining run through tools/train.py."""
 import os
 
+import numpy as np
+
 import torch
 
 from fleetx_amd.models.language_model.ernie import (ErnieModel, ErnieForPretraining,
@@ -126,3 +128,62 @@ def test_ernie_pretrain_end_to_end(tmp_path):
           "Engine.save_load.output_dir=%s" % tmp_path]
     eng = train_tool.main(["-c", cfgp] + sum([["-o", o] for o in ov], []))
     assert eng is not None
+
+
+def _pair_corpus(tmp_path):
+    """Sentence-split corpus through the offline preprocessor (GPT BPE ids)."""
+    import json
+    from tests.test_generation import _tiny_bpe
+    from fleetx_amd.data.data_tools.gpt import preprocess_data as P
+    rs = __import__("random").Random(0)
+    words = ["hello", "world", "there", "one", "two", "three", "ab", "cd"]
+    lines = []
+    for d in range(30):
+        sents = [" ".join(rs.choice(words) for _ in range(rs.randint(2, 6))) + "."
+                 for _ in range(rs.randint(2, 5))]
+        lines.append(json.dumps({"text": " ".join(sents)}))
+    (tmp_path / "c.jsonl").write_text("\n".join(lines) + "\n")
+    tok = _tiny_bpe(tmp_path / "tok")
+    prefix = str(tmp_path / "data" / "corpus")
+    P.main(["--model_name", str(tok), "--tokenizer_name", "GPTTokenizer", "--input_path",
+            str(tmp_path / "c.jsonl"), "--output_prefix", prefix, "--split_sentences"])
+    return tmp_path / "data"
+
+
+def test_ernie_sentence_pair_dataset(tmp_path):
+    from fleetx_amd.data.dataset import ErnieDataset
+    data = _pair_corpus(tmp_path)
+    ds = ErnieDataset(str(data), [1, 0, 0], 48, 200, "Train", seed=7, cls_id=509, sep_id=510,
+                      pad_id=0)
+    assert len(ds) > 0
+    nsp = []
+    for i in range(len(ds)):
+        toks, types, label, n = ds[i]
+        n = int(n)
+        assert toks[0] == 509 and toks[n - 1] == 510 and (toks[:n] == 510).sum() == 2
+        assert (toks[n:] == 0).all() and n <= 48
+        sep = int(np.nonzero(toks[:n] == 510)[0][0])
+        assert (types[:sep + 1] == 0).all() and (types[sep + 1:n] == 1).all()
+        nsp.append(int(label))
+    assert 0.2 < np.mean(nsp) < 0.8
+    a, b = ds[3], ErnieDataset(str(data), [1, 0, 0], 48, 200, "Train", seed=7, cls_id=509,
+                                   sep_id=510, pad_id=0)[3]
+    assert all(np.array_equal(x, y) for x, y in zip(a, b))  # deterministic per index
+
+
+def test_ernie_pretrain_with_nsp(tmp_path):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import train as train_tool
+    data = _pair_corpus(tmp_path)
+    cfgp = os.path.join(ROOT, "fleetx_amd/configs/nlp/ernie/pretrain_ernie_base_synthetic_dp8.yaml")
+    ov = ["Global.device=cpu", "Global.local_batch_size=4", "Global.micro_batch_size=4",
+          "Engine.max_steps=3", "Engine.logging_freq=1", "Model.vocab_size=512",
+          "Model.hidden_size=32", "Model.num_hidden_layers=2", "Model.num_attention_heads=2",
+          "Model.intermediate_size=64", "Data.Train.dataset.name=ErnieDataset",
+          "Data.Train.dataset.cls_id=509", "Data.Train.dataset.sep_id=510",
+          "Data.Train.dataset.input_dir=%s" % data, "Data.Train.dataset.split=[1,0,0]",
+          "Data.Train.dataset.max_seq_len=32", "Data.Train.loader.num_workers=0",
+          "Data.Eval=None", "Engine.save_load.output_dir=%s" % tmp_path]
+    eng = train_tool.main(["-c", cfgp] + sum([["-o", o] for o in ov], []))
+    assert eng._module.pair_data and eng._module.criterion.with_nsp_loss
