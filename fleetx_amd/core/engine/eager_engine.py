@@ -177,6 +177,10 @@ class EagerEngine(BasicEngine):
             if comm.get("overlap_optimizer", True) and not self._pipeline \
                     and self.scaler is None and hasattr(self.optimizer, "enable_forward_overlap"):
                 self.optimizer.enable_forward_overlap(model)
+            # ZeRO-1/2: the post-update parameter all-gather hides under the next forward
+            if comm.get("overlap_param_gather", True) and not self._pipeline \
+                    and hasattr(self.buffer, "enable_param_gather_overlap"):
+                self.buffer.enable_param_gather_overlap(model)
             if self._pipeline:
                 model.attach(self)
         self._profiler = self._build_profiler(configs.get("Profiler"))
@@ -421,6 +425,8 @@ class EagerEngine(BasicEngine):
             return
         if self.optimizer is not None:
             self.optimizer.sync_state()  # an overlapped update may still be in flight
+        if hasattr(self.buffer, "sync_params"):
+            self.buffer.sync_params()  # and overlapped parameter gathers
         target = self._shard_dir(ckpt.step_dir(self._output_dir, epoch, step))
         # stage 3: gather full parameters first (reference get_all_parameters, :600-601)
         with self._params_gathered():

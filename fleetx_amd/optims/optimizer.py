@@ -136,6 +136,9 @@ class FlatOptimizer:
     # ------------------------------------------------------------------ API
     def step(self):
         self._join_overlap()
+        sync = getattr(self.buffer, "sync_params", None)
+        if sync is not None:  # leftover overlapped parameter gathers of the last step
+            sync()
         self._prepare_scale()
         self.step_count += 1
         self._update(self.get_lr())

@@ -29,7 +29,10 @@ from dataclasses import asdict, dataclass
 HBM_BYTES = 288e9
 USABLE = 0.85            # leave room for the caching allocator / workspace
 SUSTAINED_FLOPS = 0.95e15  # measured: 6.7B 1-GPU step at ~38% of 2.5 PF/s
-LINK_GBPS = 50e9         # effective per-direction xGMI bandwidth per link
+# effective per-direction xGMI bandwidth per link: ~153 GB/s nominal x ~65 % RCCL
+# efficiency (an assumption -- the development box has one GPU; recalibrate from
+# SCALE_*.json once multi-GPU runs exist)
+LINK_GBPS = 100e9
 MAX_LINKS = 7            # each GPU has 7 links, one to every peer
 
 
@@ -101,10 +104,16 @@ def estimate(h, L, heads, V, s, global_batch, dp, mp, pp, sharding, stage, micro
         return None
     P = model_params(h, L, V, s)
     p_local = P / (mp * pp)
+    if stage >= 3 and pp > 1:
+        return None  # ZeRO-3 does not compose with pipeline stages here
     # ---- memory
     grads = 4.0 * p_local / (sharding if stage >= 2 else 1)
     opt = 12.0 * p_local / (sharding if stage >= 1 else 1)
     params = 2.0 * p_local
+    if stage >= 3:  # shards + two layers of full params / fp32 grads in flight
+        layer = (12.0 * h * h) / mp
+        params = 2.0 * p_local / sharding + 2 * 2.0 * layer
+        grads += 2 * 4.0 * layer
     layers_local = L // pp
     act_layer = (2.0 if recompute else 34.0 / mp) * s * micro * h
     in_flight = min(m, pp) if pp > 1 else 1  # 1F1B keeps <= pp micro-batches alive
@@ -131,8 +140,13 @@ def estimate(h, L, heads, V, s, global_batch, dp, mp, pp, sharding, stage, micro
     gbytes = 4.0 * p_local
     bucket = min(gbytes, 256e6 * 4)
     if sharding > 1:
-        grad = _rs_or_ag_s(bucket, sharding) + _rs_or_ag_s(2.0 * p_local, sharding)
-        grad += max(0.0, _rs_or_ag_s(gbytes, sharding) - comp * 0.6)
+        # fp32 grad reduce-scatter overlaps backward (~60 % of compute); the bf16
+        # parameter all-gather overlaps the next forward (~30 %); stage 3 gathers
+        # every layer twice (forward + backward) under the layer compute
+        rs = _rs_or_ag_s(gbytes, sharding)
+        ag = _rs_or_ag_s(2.0 * p_local, sharding)
+        grad = _rs_or_ag_s(bucket, sharding) + max(0.0, rs - comp * 0.6)
+        grad += max(0.0, ag - comp * 0.3) if stage < 3 else max(0.0, 2 * ag - comp * 0.8)
     else:
         grad = 0.0
     if dp > 1:
@@ -143,7 +157,15 @@ def estimate(h, L, heads, V, s, global_batch, dp, mp, pp, sharding, stage, micro
 
 
 def plan(h, L, heads, V, s, global_batch, world, allow_recompute=True, prefer=None):
-    """Best layout for ``world`` GPUs; ``prefer`` restricts to a dict of fixed degrees."""
+    """Best layout for ``world`` GPUs; ``prefer`` restricts to a dict of fixed degrees.
+    ZeRO-3 is only considered when no stage-1/2 layout fits in HBM."""
+    try:
+        return _plan(h, L, heads, V, s, global_batch, world, allow_recompute, prefer, (1, 2))
+    except ValueError:
+        return _plan(h, L, heads, V, s, global_batch, world, allow_recompute, prefer, (1, 2, 3))
+
+
+def _plan(h, L, heads, V, s, global_batch, world, allow_recompute, prefer, zero_stages):
     divs = [d for d in range(1, world + 1) if world % d == 0]
     best = None
     for mp, pp in itertools.product(divs, divs):
@@ -152,7 +174,7 @@ def plan(h, L, heads, V, s, global_batch, world, allow_recompute=True, prefer=No
         rest = world // (mp * pp)
         for sharding in [d for d in divs if rest % d == 0]:
             dp = rest // sharding
-            stages = [1, 2] if sharding > 1 else [0]
+            stages = list(zero_stages) if sharding > 1 else [0]
             for stage, recompute in itertools.product(stages, [False, True]):
                 if recompute and not allow_recompute:
                     continue

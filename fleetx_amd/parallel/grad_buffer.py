@@ -301,10 +301,73 @@ class FlatParamGradBuffer:
                     out.append((b.start + r * chunk, b.start + (r + 1) * chunk, c))
         return out
 
+    # -------------------------------------------------- overlapped parameter gather
+    _ag_need = None
+
+    def enable_param_gather_overlap(self, model):
+        """ZeRO 1/2: issue the post-update parameter all-gathers asynchronously
+        in FORWARD order and let each layer's forward pre-hook wait only for
+        the buckets holding its parameters, so the gather (bf16 params, the
+        only ZeRO traffic after the reduce-scatter that already overlaps
+        backward) hides under the next forward instead of stalling after the
+        optimizer step.  Returns False when there is nothing to overlap."""
+        if self.shard_stage < 1 or self.shard_group is None:
+            return False
+        from .sharding import find_layer_units
+        units = find_layer_units(model)
+        owner = {}
+        for i, m in enumerate(units):
+            for p in m.parameters():
+                owner.setdefault(id(p), i)
+        need = {}
+        first_use = []
+        for bi, b in enumerate(self.buckets):
+            us = [owner.get(id(p), -1) for p in b.params]
+            for u in us:
+                need.setdefault(u, set()).add(bi)
+            first_use.append(min(us))
+        self._ag_need = need
+        self._ag_order = sorted(range(len(self.buckets)), key=lambda bi: first_use[bi])
+        self._ag_works = {}
+        self._hooks.append(model.register_forward_pre_hook(self._make_ag_wait(-1)))
+        for i, m in enumerate(units):
+            self._hooks.append(m.register_forward_pre_hook(self._make_ag_wait(i)))
+        return True
+
+    def _make_ag_wait(self, unit):
+        def hook(module, args):
+            if self._ag_works:
+                for bi in self._ag_need.get(unit, ()):
+                    e = self._ag_works.pop(bi, None)
+                    if e is not None:
+                        e[0].wait()
+        return hook
+
+    def sync_params(self):
+        """Complete every outstanding overlapped parameter gather."""
+        if self._ag_need is not None:
+            for w, _ in self._ag_works.values():
+                w.wait()
+            self._ag_works = {}
+
+    def _allgather_async(self):
+        n, r = self.shard_group.nranks, self.shard_group.rank
+        self.sync_params()
+        for bi in self._ag_order:
+            b = self.buckets[bi]
+            chunk = (b.end - b.start) // n
+            full = self.param_flat[b.start:b.end]
+            mine = full[r * chunk:(r + 1) * chunk].clone()
+            w = dist.all_gather_into_tensor(full, mine, group=self.shard_group.group,
+                                            async_op=True)
+            self._ag_works[bi] = (w, mine)  # keep the send buffer alive until waited
+
     def allgather_params(self):
         """After a sharded update, every rank gathers the full model-dtype params."""
         if self.shard_stage < 1 or self.shard_group is None:
             return
+        if self._ag_need is not None:
+            return self._allgather_async()
         n = self.shard_group.nranks
         r = self.shard_group.rank
         gloo = _is_gloo(self.shard_group)

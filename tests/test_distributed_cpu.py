@@ -130,6 +130,11 @@ def test_hybrid_tp_pp_dp(ref_losses):
     _check(dist_utils.run(_train, 8, (2, 2, 2, 1, 0, 2, False, 1)), ref_losses)
 
 
+def test_sharding_stage1_dp_accumulation(ref_losses):
+    # dp2 x sharding2 ZeRO-1, two micro-batches per rank, overlapped param gather
+    _check(dist_utils.run(_train, 4, (2, 1, 1, 2, 1, 1, False, 1)), ref_losses)
+
+
 # ---------------------------------------------------------------- ZeRO stage 3
 def test_sharding_stage3(ref_losses):
     _check(dist_utils.run(_train, 2, (1, 1, 1, 2, 3, 4, False, 1)), ref_losses)
