@@ -59,6 +59,7 @@ int fx_gn_bwd_reduce(int, const void*, const void*, const float*, const float*, 
 int fx_gn_bwd_apply(int, const void*, const void*, const float*, const float*, const float*,
                     const float*, const float*, const float*, const float*, const float*, void*,
                     int, int, int, long, int, int, hipStream_t);
+int fx_transpose16(int, const void*, void*, float*, int, int, long, long, hipStream_t);
 int fx_decode_attn(const void*, const void*, const void*, void*, const int*, int, int, int, int,
                    int, long, long, long, long, long, long, float, hipStream_t);
 }
@@ -198,6 +199,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("absmax", [](int dt, ptr x, long n, ptr out, ptr st) {
     fx_absmax(dt, CP(x), n, F(out), S(st));
   });
+  m.def("transpose16", [](int dt, ptr x, ptr y, ptr part, int R, int C, long ldx, long ldy,
+                          ptr st) { return fx_transpose16(dt, CP(x), P(y), F(part), R, C, ldx, ldy, S(st)); });
   m.def("decode_attn", [](ptr q, ptr kc, ptr vc, ptr out, ptr lens, int B, int H, int D,
                           int maxlen, int nsplit, long sqb, long sqh, long skb, long sks, long skh,
                           long sob, float scale, ptr st) {

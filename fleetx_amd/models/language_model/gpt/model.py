@@ -243,6 +243,13 @@ class GPTForPretraining(nn.Module):
         super().__init__()
         self.cfg = cfg
         self.gpt = GPTModel(cfg)
+        emb = self.gpt.embeddings
+        if emb is not None:
+            # the tied word embedding gets two fused fp32 grad contributions per
+            # step (lookup backward + LM-head wgrad), both straight into main_grad
+            emb.word_embeddings.weight._fx_fused_wgrad_ok = True
+            emb.word_embeddings.weight._fx_grad_parts = 2
+            emb.position_embeddings._fx_fused_wgrad_ok = True
 
     def forward(self, input_ids, position_ids=None):
         h = self.gpt(input_ids, position_ids)

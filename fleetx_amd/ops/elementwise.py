@@ -158,3 +158,48 @@ def dropout(x, p, key):
 
 
 __all__ = ["bias_gelu", "bias_dropout_add", "dropout", "col_sum"]
+
+
+def transpose2d(x, out=None, colsum=None):
+    """``x.t().contiguous()`` for a 2-D 16-bit tensor via the LDS-tiled HIP
+    transpose (csrc/kernels/layout.hip); rows may be strided (``x.stride(1)``
+    must be 1).  CPU tensors and shapes that are not multiples of 8 use
+    PyTorch's copy.
+
+    ``colsum``: optional ``(out_f32, accumulate)`` -- the fp32 column sums of
+    ``x`` (a bias gradient) are written to / added into ``out_f32`` as a side
+    product of the same pass."""
+    if x.dim() != 2:
+        raise ValueError("transpose2d expects a 2-D tensor")
+    R, C = x.shape
+    if out is None:
+        out = torch.empty((C, R), dtype=x.dtype, device=x.device)
+    if not _lib.on_gpu(x) or x.dtype not in (torch.bfloat16, torch.float16) or x.stride(1) != 1 \
+            or (R | C | x.stride(0)) % 8 or not out.is_contiguous() \
+            or x.data_ptr() % 16 or out.data_ptr() % 16:
+        out.copy_(x.t())
+        if colsum is not None:
+            dst, acc = colsum
+            s = x.float().sum(0)
+            if acc:
+                dst.add_(s.view_as(dst))
+            else:
+                dst.copy_(s.view_as(dst))
+        return out
+    k = _lib.kernels()
+    part = None
+    if colsum is not None:
+        part = torch.empty(((R + 63) // 64, C), device=x.device, dtype=torch.float32)
+    dc = _lib.dt_code(x.dtype)
+    rc = k.transpose16(dc, _lib.ptr(x), _lib.ptr(out), _lib.ptr(part), R, C, x.stride(0), R,
+                       _lib.stream())
+    if rc != 0:
+        raise RuntimeError("transpose16 launch failed ({})".format(rc))
+    if colsum is not None:
+        dst, acc = colsum
+        if dst.dtype != torch.float32 or not dst.is_contiguous():
+            raise ValueError("colsum target must be contiguous fp32")
+        k.coltile_finalize(dc, part.data_ptr(), part.shape[0], C, dst.data_ptr(), 0, int(acc),
+                           _lib.stream())
+    _lib.maybe_sync()
+    return out

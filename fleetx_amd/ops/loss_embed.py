@@ -83,6 +83,26 @@ def softmax_cross_entropy(logits, labels, group=None, vocab_start=0, ignore_inde
     return _SoftmaxCE.apply(logits, labels, group, vocab_start, ignore_index, inplace_backward)
 
 
+def _grad_target(p, shape, device):
+    """fp32 buffer the scatter-add kernel accumulates into: the parameter's
+    flat-buffer ``main_grad`` when it takes fused gradients (no bf16 round
+    trip, no extra 4 B/elt copy), else a fresh zeroed tensor."""
+    if p is not None and getattr(p, "_fx_fused_wgrad", False) and hasattr(p, "main_grad"):
+        if getattr(p, "_fx_fresh", False):
+            p.main_grad.zero_()
+            p._fx_fresh = False
+        return p.main_grad, True
+    return torch.zeros(*shape, device=device, dtype=torch.float32), False
+
+
+def _grad_finish(p, g32, fused, dtype):
+    if fused:
+        from ..parallel.linear import grad_part_done
+        grad_part_done(p)
+        return None
+    return g32.to(dtype)
+
+
 class _Embedding(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, weight, pos_ids, pos_weight, vocab_start):
@@ -108,6 +128,7 @@ class _Embedding(torch.autograd.Function):
         ctx.pos_rows = pos_weight.shape[0] if pos_weight is not None else 0
         ctx.save_for_backward(ids_c, pos_c)
         ctx.wdtype = weight.dtype
+        ctx.params = (weight, pos_weight)
         return out.view(*ids.shape, h)
 
     @staticmethod
@@ -121,25 +142,27 @@ class _Embedding(torch.autograd.Function):
             k = _lib.kernels()
             dc = _lib.dt_code(d.dtype)
             st = _lib.stream()
-            dw32 = torch.zeros(ctx.vsize, h, device=d.device, dtype=torch.float32)
+            wp, pp = ctx.params
+            dw32, fused = _grad_target(wp, (ctx.vsize, h), d.device)
             k.embedding_bwd(dc, ids_c.data_ptr(), d.data_ptr(), dw32.data_ptr(), ntok, h,
                             int(ctx.vocab_start), ctx.vsize, st)
-            dw = dw32.to(ctx.wdtype)
+            dw = _grad_finish(wp, dw32, fused, ctx.wdtype)
             if ctx.has_pos:
-                dp32 = torch.zeros(ctx.pos_rows, h, device=d.device, dtype=torch.float32)
+                dp32, fused = _grad_target(pp, (ctx.pos_rows, h), d.device)
                 k.embedding_bwd(dc, pos_c.data_ptr(), d.data_ptr(), dp32.data_ptr(), ntok, h, 0,
                                 ctx.pos_rows, st)
-                dpos = dp32.to(ctx.wdtype)
+                dpos = _grad_finish(pp, dp32, fused, ctx.wdtype)
         else:
+            wp, pp = ctx.params
             local = ids_c - ctx.vocab_start
             inr = (local >= 0) & (local < ctx.vsize)
-            dw = torch.zeros(ctx.vsize, h, dtype=torch.float32)
-            dw.index_add_(0, local[inr], d[inr].float())
-            dw = dw.to(ctx.wdtype)
+            dw32, fused = _grad_target(wp, (ctx.vsize, h), d.device)
+            dw32.index_add_(0, local[inr], d[inr].float())
+            dw = _grad_finish(wp, dw32, fused, ctx.wdtype)
             if ctx.has_pos:
-                dpos = torch.zeros(ctx.pos_rows, h, dtype=torch.float32)
-                dpos.index_add_(0, pos_c, d.float())
-                dpos = dpos.to(ctx.wdtype)
+                dp32, fused = _grad_target(pp, (ctx.pos_rows, h), d.device)
+                dp32.index_add_(0, pos_c, d.float())
+                dpos = _grad_finish(pp, dp32, fused, ctx.wdtype)
         return None, dw, None, dpos, None
 
 

@@ -32,6 +32,8 @@ import math
 import torch
 import torch.distributed as dist
 
+from .linear import grad_part_done
+
 ALIGN = 128  # elements (256 B in bf16, 512 B in fp32)
 
 
@@ -203,7 +205,7 @@ class FlatParamGradBuffer:
                 param.main_grad.add_(g)
             param._fx_fresh = False
             param.grad = None
-            param._fx_grad_ready()
+            grad_part_done(param)
         return hook
 
     # ------------------------------------------------------------------ control

@@ -101,6 +101,8 @@ class ColumnParallelLinear(nn.Module):
                                                           dim=0, dtype=dtype, device=device,
                                                           init="zeros"))
             self.bias.tp_split = t > 1
+            # a bias applied inside linear() gets its fp32 grad from the wgrad pass
+            self.bias._fx_fused_wgrad_ok = not skip_bias_add
         else:
             self.register_parameter("bias", None)
 
@@ -188,7 +190,7 @@ def parallel_lm_logits(h, weight, parallel_output=True, sequence_parallel=False)
         h = M.all_gather_seq(h)
     else:
         h = M.copy_to_mp(h)
-    logits = F.linear(h, weight)
+    logits = linear(h, weight)  # fused fp32 wgrad into the tied weight's main_grad
     if not parallel_output:
         logits = M.gather_from_mp(logits)
     return logits

@@ -8,7 +8,17 @@ GPT-3 6.7B on one MI355X, measured with rocprofv3) plus the bf16 temporaries.
 Here the wgrad GEMM writes fp32 directly (``mm``/``addmm`` with
 ``out_dtype=float32``, beta = 0 for the first micro-batch of a step and 1
 afterwards), so the flat gradient buffer is never zero-filled either.
+
+Operand layout: the reduction of the wgrad GEMM runs over tokens, the slow
+axis of both row-major activations, and hipBLASLt's kernels for that "NT"
+case reach only ~1.0 PFLOP/s on gfx950.  On GPU both operands are first
+transposed to token-contiguous copies by the LDS-tiled HIP transpose
+(``ops.elementwise.transpose2d``) so the GEMM runs as "TN" (~1.35 PFLOP/s
+with fp32 accumulate; ``tools/bench_gemm.py``).  ``FLEETX_WGRAD_TN=0``
+restores the direct call.
 """
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -23,11 +33,55 @@ def _mm_out_supported():
     return _MM_DTYPE_OUT
 
 
-def accumulate_wgrad(weight, dy2, x2):
-    """``weight.main_grad (+)= dy2^T @ x2`` in fp32; notifies the grad buffer."""
+_WGRAD_TN = os.environ.get("FLEETX_WGRAD_TN", "1") == "1"
+
+
+def _fused(p):
+    return p is not None and getattr(p, "_fx_fused_wgrad", False) and hasattr(p, "main_grad")
+
+
+def _tn_operands(dy2, x2, colsum=None):
+    """(dy2^T, x2) as (token-contiguous dyT, xT^T view) when the TN path applies;
+    ``colsum`` = (fp32 target, accumulate) takes dy2's column sums on the way."""
+    if not (_WGRAD_TN and dy2.is_cuda and dy2.dtype in (torch.bfloat16, torch.float16)
+            and x2.dtype == dy2.dtype):
+        return None
+    from ..ops.elementwise import transpose2d
+    M = dy2.shape[0]
+    if M % 8 or dy2.shape[1] % 8 or x2.shape[1] % 8 or M < 256:
+        return None
+    return transpose2d(dy2, colsum=colsum), transpose2d(x2).t()
+
+
+def accumulate_wgrad(weight, dy2, x2, bias=None):
+    """``weight.main_grad (+)= dy2^T @ x2`` in fp32; notifies the grad buffer.
+
+    With ``bias`` (a Parameter) the bias gradient ``sum_rows(dy2)`` is produced
+    too: straight into ``bias.main_grad`` when the bias takes fused grads
+    (returns None), else returned as a tensor for autograd."""
     mg = weight.main_grad
     fresh = getattr(weight, "_fx_fresh", False)
-    a, b = dy2.t(), x2
+    db, colsum = None, None
+    if bias is not None:
+        if _fused(bias):
+            colsum = (bias.main_grad, not getattr(bias, "_fx_fresh", False))
+        else:
+            db = torch.empty(bias.shape, device=dy2.device, dtype=torch.float32)
+            colsum = (db, False)
+    tn = _tn_operands(dy2, x2, colsum)
+    if tn is None and colsum is not None:
+        s = dy2.float().sum(0)
+        if colsum[1]:
+            colsum[0].add_(s)
+        else:
+            colsum[0].copy_(s)
+    if bias is not None:
+        if db is None:
+            bias._fx_fresh = False
+            grad_part_done(bias)
+        else:
+            db = db.to(bias.dtype)
+    a, b = tn if tn is not None else (dy2.t(), x2)
     if dy2.dtype == torch.float32:
         if fresh:
             torch.mm(a, b, out=mg)
@@ -45,7 +99,21 @@ def accumulate_wgrad(weight, dy2, x2):
         else:
             mg.add_(g)
     weight._fx_fresh = False
-    cb = getattr(weight, "_fx_grad_ready", None)
+    grad_part_done(weight)
+    return db
+
+
+def grad_part_done(p):
+    """One fused contribution to ``p.main_grad`` is in.  A weight used twice in
+    a step (the tied word embedding: lookup + LM head, ``_fx_grad_parts = 2``)
+    is reported ready to the gradient buffer only after its last part."""
+    parts = getattr(p, "_fx_grad_parts", 1)
+    if parts > 1:
+        p._fx_parts_seen = getattr(p, "_fx_parts_seen", 0) + 1
+        if p._fx_parts_seen < parts:
+            return
+        p._fx_parts_seen = 0
+    cb = getattr(p, "_fx_grad_ready", None)
     if cb is not None:
         cb()
 
@@ -54,7 +122,7 @@ class _FusedWgradLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
-        ctx.has_bias = bias is not None
+        ctx.bias = bias
         return F.linear(x, weight, bias)
 
     @staticmethod
@@ -63,8 +131,7 @@ class _FusedWgradLinear(torch.autograd.Function):
         dx = torch.matmul(dy, w)
         dy2 = dy.reshape(-1, dy.shape[-1])
         x2 = x.reshape(-1, x.shape[-1])
-        accumulate_wgrad(w, dy2, x2)
-        db = dy2.sum(0) if ctx.has_bias else None
+        db = accumulate_wgrad(w, dy2, x2, ctx.bias)
         return dx, None, db
 
 

@@ -40,6 +40,7 @@ import contextlib
 import torch
 import torch.distributed as dist
 
+from .linear import grad_part_done
 from .grad_buffer import ALIGN, Category, _is_gloo, _round_up, default_decay_fn
 
 
@@ -333,7 +334,7 @@ class Stage3ParamGradBuffer:
             param.main_grad.add_(g)
         param._fx_fresh = False
         param.grad = None
-        param._fx_grad_ready()
+        grad_part_done(param)
 
     def _make_ready(self, p):
         def ready():

@@ -530,3 +530,44 @@ def test_imagen_unet_train_step_on_gpu():
         assert torch.isfinite(loss)
     out = m.sample(text_embeds=te[:2], cond_scale=2.0)
     assert out.shape == (2, 3, 32, 32) and torch.isfinite(out).all()
+
+
+@pytest.mark.parametrize("R,C", [(64, 64), (136, 200), (8192, 1024), (24, 4104)])
+def test_transpose2d(R, C):
+    from fleetx_amd.ops.elementwise import transpose2d
+    x = torch.randn(R, C + 16, device="cuda").to(torch.bfloat16)[:, :C]  # strided rows
+    y = transpose2d(x)
+    assert y.shape == (C, R) and y.is_contiguous()
+    assert torch.equal(y, x.t().contiguous())
+    cs = torch.full((C,), 1.0, device="cuda")
+    y2 = transpose2d(x, colsum=(cs, True))
+    assert torch.equal(y2, y)
+    torch.testing.assert_close(cs, 1.0 + x.float().sum(0), rtol=1e-4, atol=1e-3)
+
+
+def test_tn_wgrad_matches_direct():
+    from fleetx_amd.parallel import linear as L
+    torch.manual_seed(0)
+    M, N, K = 2048, 384, 256
+    dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    ref = dy.float().t() @ x.float()
+    for tn in (True, False):
+        w = torch.nn.Parameter(torch.zeros(N, K, device="cuda", dtype=torch.bfloat16))
+        w.main_grad = torch.full((N, K), 7.0, device="cuda")
+        w._fx_fresh = True
+        b = torch.nn.Parameter(torch.zeros(N, device="cuda", dtype=torch.bfloat16))
+        b.main_grad = torch.full((N,), 7.0, device="cuda")
+        b._fx_fresh, b._fx_fused_wgrad = True, True
+        b2 = torch.nn.Parameter(torch.zeros(N, device="cuda", dtype=torch.bfloat16))
+        old, L._WGRAD_TN = L._WGRAD_TN, tn
+        try:
+            assert (L._tn_operands(dy, x) is not None) == tn
+            assert L.accumulate_wgrad(w, dy, x, b) is None   # fresh: overwrite
+            L.accumulate_wgrad(w, dy, x, b)                  # accumulate
+            db = L.accumulate_wgrad(w, dy, x, b2)            # unfused bias: returned
+        finally:
+            L._WGRAD_TN = old
+        torch.testing.assert_close(w.main_grad, 3 * ref, rtol=2e-3, atol=3e-2)
+        torch.testing.assert_close(b.main_grad, 2 * dy.float().sum(0), rtol=1e-3, atol=1e-2)
+        torch.testing.assert_close(db.float(), dy.float().sum(0), rtol=1e-2, atol=1e-1)

@@ -1,0 +1,81 @@
+"""GEMM micro-benchmark for the transformer-layer shapes (fwd / dgrad / wgrad)
+under the weight layouts the framework can use, sustained back-to-back like a
+training step.
+
+    python tools/bench_gemm.py [--tokens 8192 --hidden 4096 --iters 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), "..")))
+
+import torch  # noqa: E402
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tokens", type=int, default=8192)
+    ap.add_argument("--hidden", type=int, default=4096)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="", help="comma list of case names")
+    a = ap.parse_args()
+    from fleetx_amd.ops.elementwise import transpose2d
+    M, h = a.tokens, a.hidden
+    dev, bf = "cuda", torch.bfloat16
+    shapes = {"qkv": (h, 3 * h), "out": (h, h), "fc1": (h, 4 * h), "fc2": (4 * h, h)}
+    for name, (K, N) in shapes.items():
+        x = torch.randn(M, K, device=dev, dtype=bf)
+        w = torch.randn(N, K, device=dev, dtype=bf) * 0.02       # [out, in]
+        wt = w.t().contiguous()                                   # [in, out]
+        dy = torch.randn(M, N, device=dev, dtype=bf)
+        dw32 = torch.empty(N, K, device=dev, dtype=torch.float32)
+        dyT = dy.t().contiguous()                                 # [N, M]
+        xT = x.t().contiguous()                                   # [K, M]
+        fl = 2.0 * M * N * K
+        res = {"gemm": name, "M": M, "N": N, "K": K}
+        cases = {
+            "fwd_x_wT": lambda: torch.nn.functional.linear(x, w),
+            "fwd_x_wt": lambda: torch.mm(x, wt),
+            "dgrad_dy_w": lambda: torch.mm(dy, w),
+            "dgrad_dy_wtT": lambda: torch.mm(dy, wt.t()),
+            "wgrad_bf16": lambda: torch.mm(dy.t(), x),
+            "wgrad_f32out": lambda: torch.ops.aten.mm.dtype_out(dy.t(), x, torch.float32, out=dw32),
+            "wgrad_f32acc": lambda: torch.ops.aten.addmm.dtype_out(dw32, dy.t(), x, torch.float32,
+                                                                   out=dw32),
+            # wgrad as a "TN" GEMM on transposed (token-contiguous) operands
+            "wgradTN_bf16": lambda: torch.nn.functional.linear(dyT, xT),
+            "wgradTN_f32out": lambda: torch.ops.aten.mm.dtype_out(dyT, xT.t(), torch.float32,
+                                                                  out=dw32),
+            "wgradTN_f32acc": lambda: torch.ops.aten.addmm.dtype_out(dw32, dyT, xT.t(),
+                                                                     torch.float32, out=dw32),
+            "transpose_dy": lambda: dyT.copy_(dy.t()),
+            "transpose_dy_hip": lambda: transpose2d(dy, out=dyT),
+            "wgrad_tn_path": lambda: torch.ops.aten.addmm.dtype_out(
+                dw32, transpose2d(dy), transpose2d(x).t(), torch.float32, out=dw32),
+        }
+        for k, fn in cases.items():
+            if a.only and k not in a.only.split(","):
+                continue
+            ms = timeit(fn, a.iters)
+            # TFLOP/s of the GEMM (for transposes: us per call)
+            res[k] = round(ms * 1e3, 1) if k.startswith("transpose") else round(fl / ms / 1e9, 1)
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -3,6 +3,12 @@
 calls, share -- with template noise stripped from the names.
 
     python tools/kernel_summary.py trace.csv [--steps N] [--top 30] [--md out.md]
+        [--window adamw_flat:2:6]
+
+``--window NAME:A:B`` (kernel traces only) keeps the kernels that start after
+the A-th and up to the B-th completion of a kernel whose name contains NAME
+-- e.g. the optimizer kernel closes every step, so this cuts warm-up and
+start-up kernels out of a multi-step trace.
 """
 import argparse
 import collections
@@ -22,8 +28,22 @@ def short(name):
     return n[:110]
 
 
-def load(path):
+def _window(rows, spec):
+    name, a, b = spec.rsplit(":", 2)
+    a, b = int(a), int(b)
+    rows = sorted(rows, key=lambda r: float(r["Start_Timestamp"]))
+    ends = sorted(float(r["End_Timestamp"]) for r in rows if name in r["Kernel_Name"])
+    if len(ends) < b:
+        raise SystemExit("only %d '%s' kernels in the trace" % (len(ends), name))
+    lo = ends[a - 1] if a > 0 else float("-inf")
+    hi = ends[b - 1]
+    return [r for r in rows if lo < float(r["Start_Timestamp"]) <= hi]
+
+
+def load(path, window=None):
     rows = list(csv.DictReader(open(path)))
+    if window:
+        rows = _window(rows, window)
     agg = collections.defaultdict(lambda: [0.0, 0])
     if rows and "TotalDurationNs" in rows[0]:
         for r in rows:
@@ -44,8 +64,9 @@ def main():
     ap.add_argument("--steps", type=float, default=1.0, help="divide totals by this many steps")
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--md", default=None)
+    ap.add_argument("--window", default=None)
     a = ap.parse_args()
-    agg = load(a.csv)
+    agg = load(a.csv, a.window)
     total = sum(v[0] for v in agg.values())
     lines = ["| kernel | ms/step | calls/step | share |", "|---|---:|---:|---:|"]
     for k, (ns, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:a.top]:
