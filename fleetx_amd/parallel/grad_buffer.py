@@ -28,6 +28,7 @@ MI355X design:
   communication overlaps the rest of backward on RCCL's stream.
 """
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -77,6 +78,11 @@ class Bucket:
 
 
 def _is_gloo(g):
+    """gloo stand-ins for the RCCL collective forms; ``FLEETX_GLOO_AS_RCCL=1``
+    disables them so CPU tests exercise the exact in-place reduce-scatter /
+    all-gather-into-tensor code the GPU path runs."""
+    if os.environ.get("FLEETX_GLOO_AS_RCCL", "0") == "1":
+        return False
     try:
         return dist.get_backend(g.group) == "gloo"
     except Exception:

@@ -207,3 +207,13 @@ def test_sharding_stage3_memory_and_resume(tmp_path):
         for a, b in zip(r["cont"], r["res"]):
             assert abs(a - b) < 1e-6, (r["cont"], r["res"])
     assert (tmp_path / "epoch_0_step_2" / "mp_00_sharding_01_pp_00" / "model.pdparams").exists()
+
+
+# ------------------------------------------- RCCL collective forms on gloo
+@pytest.mark.parametrize("stage,dp,micro", [(1, 1, 4), (2, 1, 4), (3, 1, 4), (1, 2, 1)])
+def test_sharding_rccl_collective_forms(ref_losses, monkeypatch, stage, dp, micro):
+    """The in-place reduce_scatter_tensor / all_gather_into_tensor calls the
+    RCCL path issues (gloo otherwise takes all_reduce stand-ins)."""
+    monkeypatch.setenv("FLEETX_GLOO_AS_RCCL", "1")
+    world = 2 * dp
+    _check(dist_utils.run(_train, world, (dp, 1, 1, 2, stage, micro, False, 1)), ref_losses)
