@@ -60,6 +60,8 @@ int fx_gn_bwd_apply(int, const void*, const void*, const float*, const float*, c
                     const float*, const float*, const float*, const float*, const float*, void*,
                     int, int, int, long, int, int, hipStream_t);
 int fx_transpose16(int, const void*, void*, float*, int, int, long, long, hipStream_t);
+int fx_sample(int, const void*, long, int, int, float, int, float, const float*, int64_t*, float*,
+              float*, hipStream_t);
 int fx_decode_attn(const void*, const void*, const void*, void*, const int*, int, int, int, int,
                    int, long, long, long, long, long, long, float, hipStream_t);
 }
@@ -201,6 +203,11 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.def("transpose16", [](int dt, ptr x, ptr y, ptr part, int R, int C, long ldx, long ldy,
                           ptr st) { return fx_transpose16(dt, CP(x), P(y), F(part), R, C, ldx, ldy, S(st)); });
+  m.def("sample", [](int dt, ptr logits, long ld, int B, int V, float inv_temp, int top_k,
+                     float top_p, ptr u, ptr ids, ptr lse, ptr probs, ptr st) {
+    return fx_sample(dt, CP(logits), ld, B, V, inv_temp, top_k, top_p, F(u),
+                     reinterpret_cast<int64_t*>(ids), F(lse), F(probs), S(st));
+  });
   m.def("decode_attn", [](ptr q, ptr kc, ptr vc, ptr out, ptr lens, int B, int H, int D,
                           int maxlen, int nsplit, long sqb, long sqh, long skb, long sks, long skh,
                           long sob, float scale, ptr st) {

@@ -315,18 +315,25 @@ class GPTForGeneration(torch.nn.Module):
                 if hasattr(pr, "cur_len"):
                     pr.cur_len = step
             logits = procs(history, logits)
-            logp = torch.log_softmax(logits, -1)
-            if self.decode_strategy == "greedy_search":
-                nxt = torch.argmax(logits, -1)
+            if self.decode_strategy != "greedy_search" and logits.is_cuda:
+                # one fused HIP launch: softmax/T, top-k, top-p, draw, logsumexp
+                nxt, lse = ops.fused_sample(logits, self.temperature, self.top_k, self.top_p,
+                                            generator=gen)
+                step_score = logits.gather(1, nxt[:, None]).squeeze(1).float() - lse
             else:
-                lg = logits / self.temperature if self.temperature not in (None, 1.0) else logits
-                probs = torch.softmax(lg, -1)
-                if self.top_k:
-                    probs = top_k_filter(probs, self.top_k)
-                if self.top_p is not None and self.top_p < 1.0:
-                    probs = top_p_filter(probs, self.top_p)
-                nxt = torch.multinomial(probs, 1, generator=gen).squeeze(1)
-            step_score = logp.gather(1, nxt[:, None]).squeeze(1)
+                logp = torch.log_softmax(logits, -1)
+                if self.decode_strategy == "greedy_search":
+                    nxt = torch.argmax(logits, -1)
+                else:
+                    lg = logits / self.temperature if self.temperature not in (None, 1.0) \
+                        else logits
+                    probs = torch.softmax(lg, -1)
+                    if self.top_k:
+                        probs = top_k_filter(probs, self.top_k)
+                    if self.top_p is not None and self.top_p < 1.0:
+                        probs = top_p_filter(probs, self.top_p)
+                    nxt = torch.multinomial(probs, 1, generator=gen).squeeze(1)
+                step_score = logp.gather(1, nxt[:, None]).squeeze(1)
             nxt = torch.where(unfinished, nxt, torch.full_like(nxt, pad))
             scores = torch.where(unfinished, scores + step_score, scores)
             out_tokens.append(nxt)

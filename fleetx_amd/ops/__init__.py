@@ -5,5 +5,6 @@ from .attention import (flash_attention, flash_attention_qkvpacked, attention_re
                         decode_attention)
 from .loss_embed import softmax_cross_entropy, embedding  # noqa: F401
 from .quant import fake_quant  # noqa: F401
+from .sampling import fused_sample  # noqa: F401
 from . import _lib  # noqa: F401
 from .groupnorm import group_norm_silu, GroupNormSiLU  # noqa: F401,E402

@@ -571,3 +571,44 @@ def test_tn_wgrad_matches_direct():
         torch.testing.assert_close(w.main_grad, 3 * ref, rtol=2e-3, atol=3e-2)
         torch.testing.assert_close(b.main_grad, 2 * dy.float().sum(0), rtol=1e-3, atol=1e-2)
         torch.testing.assert_close(db.float(), dy.float().sum(0), rtol=1e-2, atol=1e-1)
+
+
+# ---------------------------------------------------------------- fused sampling (K18)
+@pytest.mark.parametrize("T,k,p", [(1.0, 50, 1.0), (0.7, 0, 0.9), (0.8, 40, 0.8), (1.3, 0, 1.0)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fused_sample_filter_matches_reference(T, k, p, dtype):
+    from fleetx_amd.ops import fused_sample
+    from fleetx_amd.models.language_model.gpt.generation import top_k_filter, top_p_filter
+    logits = (torch.randn(4, 50304, device="cuda") * 3).to(dtype)
+    ids, lse, probs = fused_sample(logits, T, k, p, return_probs=True)
+    ref = torch.softmax(logits.float() / T, -1)
+    if k:
+        ref = top_k_filter(ref, k)
+    if p < 1.0:
+        ref = top_p_filter(ref, p)
+    diff = (probs > 0) != (ref > 0)
+    if diff.any():
+        # only ties at the nucleus boundary (bf16 logits repeat values) may differ:
+        # the kernel keeps every token equal to the threshold, a sort cuts inside the tie
+        assert dtype == torch.bfloat16 and p < 1.0
+        kmin = torch.where(probs > 0, probs, torch.full_like(probs, 2.0)).min(-1, keepdim=True).values
+        assert torch.allclose(probs[diff], kmin.expand_as(probs)[diff], rtol=1e-6)
+        ref = torch.where(diff, probs, ref)
+    torch.testing.assert_close(probs, ref, rtol=1e-4, atol=1e-7)
+    torch.testing.assert_close(lse, torch.logsumexp(logits.float(), -1), rtol=1e-5, atol=1e-4)
+    assert bool((ref.gather(1, ids[:, None]) > 0).all())  # drawn tokens survive the filters
+
+
+def test_fused_sample_greedy_and_distribution():
+    from fleetx_amd.ops import fused_sample
+    logits = torch.randn(8, 1000, device="cuda")
+    ids, _ = fused_sample(logits, 1.0, 1, 1.0)
+    assert torch.equal(ids, logits.argmax(-1))
+    ids, _ = fused_sample(logits, 1.0, 0, 1e-6)  # nucleus of one token
+    assert torch.equal(ids, logits.argmax(-1))
+    row = torch.randn(1, 24, device="cuda")
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    ids, _ = fused_sample(row.expand(40000, 24).contiguous(), 1.0, 0, 1.0, generator=g)
+    freq = torch.bincount(ids, minlength=24).float() / ids.numel()
+    assert (freq - torch.softmax(row[0], -1)).abs().max().item() < 0.01
