@@ -114,6 +114,8 @@ def main():
           "Engine.save_load.save_steps=-1", "Engine.mix_precision.dtype=bfloat16",
           "Data.Train.dataset.max_seq_len=%d" % args.seq,
           "Data.Train.dataset.name=SyntheticGPTDataset"]
+    # A/B experiments: extra config overrides, e.g. "Distributed.comm.early_grad_norm=False"
+    ov += [o for o in os.environ.get("FLEETX_BENCH_OVERRIDES", "").split(";") if o]
     os.environ.setdefault("FLEETX_LOG_RANK0_ONLY", "1")
     cfg = cfgmod.get_config(cfg_file, overrides=ov, nranks=n)
     env.init_dist_env(cfg)

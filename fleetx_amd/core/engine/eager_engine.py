@@ -177,6 +177,11 @@ class EagerEngine(BasicEngine):
             if comm.get("overlap_optimizer", True) and not self._pipeline \
                     and self.scaler is None and hasattr(self.optimizer, "enable_forward_overlap"):
                 self.optimizer.enable_forward_overlap(model)
+            # single data rank: gradient sum-of-squares per bucket under backward
+            # (opt-in: measured neutral on 6.7B, the GEMMs leave no CU slots free)
+            if comm.get("early_grad_norm", False) and not self._pipeline \
+                    and hasattr(self.buffer, "enable_early_norm"):
+                self.buffer.enable_early_norm()
             # ZeRO-1/2: the post-update parameter all-gather hides under the next forward
             if comm.get("overlap_param_gather", True) and not self._pipeline \
                     and hasattr(self.buffer, "enable_param_gather_overlap"):

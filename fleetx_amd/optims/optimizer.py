@@ -94,16 +94,22 @@ class FlatOptimizer:
     def compute_grad_norm(self):
         """Global L2 norm over the data/model-parallel world (device scalar)."""
         dev = self.buffer.device
-        dist_sq = torch.zeros((), dtype=torch.float32, device=dev)
-        rep_sq = torch.zeros((), dtype=torch.float32, device=dev)
-        for (s, e, c), g in zip(self.ranges, self.grad_views()):
-            if c.norm_excluded:
-                continue
-            sq = _sumsq(g)
-            if c.distributed:
-                dist_sq = dist_sq + sq
-            else:
-                rep_sq = rep_sq + sq
+        early = getattr(self.buffer, "early_norm", None)
+        if early is not None:
+            # per-bucket sums taken on a side stream during backward
+            dist_sq, rep_sq = early
+            self.buffer.early_norm = None
+        else:
+            dist_sq = torch.zeros((), dtype=torch.float32, device=dev)
+            rep_sq = torch.zeros((), dtype=torch.float32, device=dev)
+            for (s, e, c), g in zip(self.ranges, self.grad_views()):
+                if c.norm_excluded:
+                    continue
+                sq = _sumsq(g)
+                if c.distributed:
+                    dist_sq = dist_sq + sq
+                else:
+                    rep_sq = rep_sq + sq
         shard = self.buffer.shard_group if self.buffer.shard_stage >= 1 else None
         if shard is not None:
             pair = torch.stack([dist_sq, rep_sq])

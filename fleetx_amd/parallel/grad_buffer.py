@@ -172,6 +172,8 @@ class FlatParamGradBuffer:
         self._hooks = []
         self._accumulating = True
         self._last_micro = True
+        self._norm_stream = None
+        self.early_norm = None
         self._install_hooks()
 
     # ------------------------------------------------------------------ setup
@@ -230,6 +232,48 @@ class FlatParamGradBuffer:
             b.work = None
             b.launched = False
 
+    # ------------------------------------------------------------------ early grad norm
+    def enable_early_norm(self):
+        """Sum of squares of each bucket as soon as it is final, on a side
+        stream under the rest of backward (single data rank only: with data
+        parallel / ZeRO the norm is over reduced, owned grads).  The optimizer
+        reads ``early_norm`` instead of re-reading every gradient after
+        backward (~4.6 ms for 6.7B on one MI355X)."""
+        if self.device.type != "cuda" or self.dp_group is not None or \
+                self.shard_group is not None or not self.overlap or self.embed_group is not None:
+            return False
+        if self.mp_group is not None and any(c.seq_parallel for c in self.categories):
+            return False  # finish() all-reduces those grads over mp after the buckets
+        self._norm_stream = torch.cuda.Stream(device=self.device)
+        self._norm_part = torch.zeros(len(self.buckets), dtype=torch.float32, device=self.device)
+        self._bucket_index = {id(b): i for i, b in enumerate(self.buckets)}
+        cat_of = []
+        for b in self.buckets:
+            c = next(c for c in self.categories if c.start <= b.start < c.end)
+            cat_of.append(c)
+        self._norm_dist_idx = torch.tensor(
+            [i for i, c in enumerate(cat_of) if c.distributed and not c.norm_excluded],
+            dtype=torch.long, device=self.device)
+        self._norm_rep_idx = torch.tensor(
+            [i for i, c in enumerate(cat_of) if not c.distributed and not c.norm_excluded],
+            dtype=torch.long, device=self.device)
+        return True
+
+    def _early_norm_bucket(self, b):
+        from ..optims.optimizer import _sumsq
+        ev = torch.cuda.Event()
+        ev.record()
+        with torch.cuda.stream(self._norm_stream):
+            self._norm_stream.wait_event(ev)
+            i = self._bucket_index[id(b)]
+            self._norm_part[i:i + 1].copy_(_sumsq(self.grad_flat[b.start:b.end]).reshape(1))
+
+    def _finish_early_norm(self):
+        """(distributed_sq, replicated_sq) device scalars, joined to the current stream."""
+        torch.cuda.current_stream().wait_stream(self._norm_stream)
+        part = self._norm_part
+        self.early_norm = (part[self._norm_dist_idx].sum(), part[self._norm_rep_idx].sum())
+
     def _data_groups(self):
         return self.dp_group, self.shard_group
 
@@ -239,6 +283,8 @@ class FlatParamGradBuffer:
         b.launched = True
         seg = self.grad_flat[b.start:b.end]
         works = []
+        if self._norm_stream is not None:  # _launch only runs on final gradients
+            self._early_norm_bucket(b)
         if self.shard_stage >= 1 and self.shard_group is not None:
             # reduce-scatter to the owner (in place: RCCL's recvbuff = sendbuff + rank*count);
             # dp all-reduce of the owned shard follows in finish()
@@ -290,6 +336,8 @@ class FlatParamGradBuffer:
             for n, p in self.params:
                 if getattr(p, "shared_embedding", False):
                     dist.all_reduce(p.main_grad, group=self.embed_group.group)
+        if self._norm_stream is not None:
+            self._finish_early_norm()
         for b in self.buckets:
             b.launched = False
             b.work = None

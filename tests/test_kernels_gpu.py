@@ -612,3 +612,37 @@ def test_fused_sample_greedy_and_distribution():
     ids, _ = fused_sample(row.expand(40000, 24).contiguous(), 1.0, 0, 1.0, generator=g)
     freq = torch.bincount(ids, minlength=24).float() / ids.numel()
     assert (freq - torch.softmax(row[0], -1)).abs().max().item() < 0.01
+
+
+def test_early_grad_norm_matches_post_backward_norm():
+    """Per-bucket sum of squares on a side stream under backward == the
+    post-backward norm pass; training curves identical."""
+    from fleetx_amd.models.language_model.gpt.model import (GPTConfig, GPTForPretraining,
+                                                            GPTPretrainingCriterion)
+    from fleetx_amd.parallel.grad_buffer import FlatParamGradBuffer
+    from fleetx_amd.optims.optimizer import FusedAdamW, ClipGradByGlobalNorm
+    toks = torch.randint(0, 2048, (4, 257), device=DEV)
+    runs = []
+    for early in (False, True):
+        torch.manual_seed(0)
+        cfg = GPTConfig(vocab_size=2048, hidden_size=256, num_layers=4, num_attention_heads=4,
+                        max_position_embeddings=256, dtype=torch.bfloat16,
+                        hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+        model = GPTForPretraining(cfg).cuda()
+        crit = GPTPretrainingCriterion(cfg)
+        buf = FlatParamGradBuffer(model.named_parameters(), bucket_mb=1)
+        assert buf.enable_early_norm() if early else True
+        assert len(buf.buckets) > 3
+        opt = FusedAdamW(2e-3, buf, grad_clip=ClipGradByGlobalNorm(0.5))
+        norms = []
+        for _ in range(3):
+            loss = crit(model(toks[:, :-1]), toks[:, 1:], torch.ones(4, 256, device=DEV))
+            loss.backward()
+            buf.finish()
+            assert (buf.early_norm is not None) == early
+            opt.step()
+            opt.clear_grad()
+            norms.append(float(opt.last_grad_norm))
+        runs.append(norms)
+    for a, b in zip(*runs):
+        assert abs(a - b) <= 1e-4 * a, runs
