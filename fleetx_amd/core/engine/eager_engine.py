@@ -38,6 +38,9 @@ from ...parallel.rng import get_rng_state_tracker
 from ...utils import checkpoint as ckpt
 from ...utils import env
 from ...utils.log import logger
+from ...utils.profiler import phase
+
+_END = object()
 
 
 class DynamicLossScaler:
@@ -221,13 +224,17 @@ class EagerEngine(BasicEngine):
             loss = None
             for i, mb in enumerate(micro):
                 self.buffer.set_last_micro_batch(i == len(micro) - 1)
-                l = self._module.training_step(mb)
-                if self._accumulate_steps > 1:
-                    l = l / self._accumulate_steps
-                self._module.backward(l * self.scaler.scale if self.scaler is not None else l)
+                with phase("Forward"):
+                    l = self._module.training_step(mb)
+                    if self._accumulate_steps > 1:
+                        l = l / self._accumulate_steps
+                with phase("Backward"):
+                    self._module.backward(l * self.scaler.scale if self.scaler is not None else l)
                 loss = l.detach() if loss is None else loss + l.detach()
-        self.buffer.finish()
-        self._optim_update()
+        with phase("GradSync"):
+            self.buffer.finish()
+        with phase("Optimization"):
+            self._optim_update()
         return loss
 
     def _optim_update(self):
@@ -273,9 +280,14 @@ class EagerEngine(BasicEngine):
         total = _safe_len(loader)
         loss_acc, n_acc = None, 0
         t0 = time.time()
-        for batch in loader:
+        it = iter(loader)
+        while True:
+            with phase("Dataloader"):
+                batch = next(it, _END)
+                if batch is _END:
+                    break
+                batch = _to_device(batch, self.device)
             self._fault_check(global_step)
-            batch = _to_device(batch, self.device)
             loss = self._fit_impl(batch)
             global_step += 1
             self.consumed_samples += gbs

@@ -136,3 +136,26 @@ def test_train_cli_cpu_fp32(tmp_path):
     recs = [json.loads(l) for l in open(tmp_path / "metrics.jsonl")]
     assert [r["step"] for r in recs] == [1, 2, 3, 4]
     assert all(r["tokens_per_s"] > 0 and "grad_norm" in r and "lr" in r for r in recs)
+
+
+def test_profiler_views(tmp_path):
+    """Profiler YAML block -> Chrome trace + Overview/Model/Kernel/Operator/
+    Distributed views with the engine's phases (reference §5.1)."""
+    class _Loader:
+        def __iter__(self):
+            return iter([_batch(i) for i in range(6)])
+
+        def __len__(self):
+            return 6
+
+    e, _ = _engine(tmp_path, ["Profiler.enable=True", "Profiler.scheduler=[2,4]",
+                              "Profiler.profiler_log=%s" % (tmp_path / "prof"),
+                              "Engine.max_steps=5", "Engine.logging_freq=1000"])
+    e.fit(epoch=1, train_data_loader=_Loader())
+    text = (tmp_path / "prof" / "summary_rank0.txt").read_text()
+    for view in ("Overview Summary", "Model Summary", "Kernel Summary", "Operator Summary",
+                 "Distributed Summary"):
+        assert view in text
+    for ph in ("Dataloader", "Forward", "Backward", "GradSync", "Optimization"):
+        assert ph in text.split("Model Summary")[1].split("Kernel Summary")[0], text
+    assert any(p.name.startswith("trace_rank0") for p in (tmp_path / "prof").iterdir())

@@ -646,3 +646,40 @@ def test_early_grad_norm_matches_post_backward_norm():
         runs.append(norms)
     for a, b in zip(*runs):
         assert abs(a - b) <= 1e-4 * a, runs
+
+
+def test_profiler_kernel_view_shows_hip_kernels(tmp_path):
+    from tests.test_engine_cpu import CFG
+    from fleetx_amd.utils import config as C
+    from fleetx_amd.utils import env
+    from fleetx_amd.models import build_module
+    from fleetx_amd.core.engine.eager_engine import EagerEngine
+    ov = ["Model.hidden_size=256", "Model.num_layers=2", "Model.num_attention_heads=4",
+          "Model.vocab_size=1024", "Model.max_position_embeddings=256",
+          "Global.local_batch_size=4", "Global.micro_batch_size=4", "Engine.max_steps=5",
+          "Engine.logging_freq=1000", "Engine.mix_precision.dtype=bfloat16",
+          "Engine.save_load.output_dir=%s" % tmp_path, "Data.Train.dataset.max_seq_len=256",
+          "Data.Train.dataset.name=SyntheticGPTDataset", "Profiler.enable=True",
+          "Profiler.scheduler=[2,4]", "Profiler.profiler_log=%s" % (tmp_path / "prof")]
+    cfg = C.get_config(CFG, overrides=ov, nranks=1)
+    env.set_seed(cfg.Global.seed)
+    eng = EagerEngine(configs=cfg, module=build_module(cfg), mode="train")
+    g = torch.Generator().manual_seed(0)
+
+    class _Loader:
+        def __iter__(self):
+            for _ in range(6):
+                t = torch.randint(0, 1024, (4, 257), generator=g)
+                yield [t[:, :-1].contiguous(), torch.arange(256).expand(4, 256).contiguous(),
+                       t[:, 1:].contiguous(), torch.ones(4, 256)]
+
+        def __len__(self):
+            return 6
+
+    eng.fit(epoch=1, train_data_loader=_Loader())
+    text = (tmp_path / "prof" / "summary_rank0.txt").read_text()
+    kern = text.split("Kernel Summary")[1].split("Operator Summary")[0]
+    assert "fa_fwd_kernel" in kern and "adamw_flat_kernel" in kern, text
+    model = text.split("Model Summary")[1].split("Kernel Summary")[0]
+    fwd = [l for l in model.splitlines() if l.startswith("Forward")][0]
+    assert float(fwd.split("|")[3]) > 0.0, model  # device time attributed to the phase
