@@ -26,7 +26,8 @@ import torch
 
 from .log import logger
 
-_PHASES = {"profiling": False, "roctx": os.environ.get("FLEETX_ROCTX", "0") == "1"}
+_PHASES = {"profiling": False, "roctx": os.environ.get("FLEETX_ROCTX", "0") == "1",
+           "marks": []}
 
 PHASE_PREFIX = "FX::"
 PHASES = ("Dataloader", "Forward", "Backward", "GradSync", "Optimization")
@@ -41,6 +42,13 @@ def phase(name):
         return
     if on_tx and torch.cuda.is_available():
         torch.cuda.nvtx.range_push(name)  # roctx on ROCm builds
+    ev = None
+    if on_prof and torch.cuda.is_available():
+        # device-side span of the phase on the compute stream (autograd's
+        # backward kernels are launched from another thread, so the
+        # profiler's GPU annotations cannot attribute them)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
     try:
         if on_prof:
             with torch.profiler.record_function(PHASE_PREFIX + name):
@@ -48,6 +56,9 @@ def phase(name):
         else:
             yield
     finally:
+        if ev is not None:
+            ev[1].record()
+            _PHASES["marks"].append((name, ev[0], ev[1]))
         if on_tx and torch.cuda.is_available():
             torch.cuda.nvtx.range_pop()
 
@@ -70,7 +81,8 @@ def _self_dev_time(e):
 
 def _is_kernel(e):
     dt = getattr(e, "device_type", None)
-    return dt is not None and dt == torch.autograd.DeviceType.CUDA
+    return dt is not None and dt == torch.autograd.DeviceType.CUDA and \
+        not e.name.startswith(PHASE_PREFIX) and not e.name.startswith("ProfilerStep")
 
 
 def _union(intervals):
@@ -124,14 +136,23 @@ def _table(title, header, rows):
     return "\n".join(out)
 
 
+def _short(name):
+    n = name.replace("(anonymous namespace)::", "")
+    if n.startswith("void "):
+        n = n[5:]
+    i = n.find("(")
+    return n[:i] if i > 0 else n
+
+
 def _is_comm(name):
     n = name.lower()
     return "nccl" in n or "rccl" in n or "allreduce" in n or "all_reduce" in n or \
         "reducescatter" in n or "allgather" in n
 
 
-def summarize(events, views=None, steps=1, memory=False, top=25):
-    """Text views over a ``torch.profiler`` event list (times in ms)."""
+def summarize(events, views=None, steps=1, memory=False, top=25, device_phase_ms=None):
+    """Text views over a ``torch.profiler`` event list (times in ms);
+    ``device_phase_ms``: {phase: device-stream span} from :func:`phase` marks."""
     views = dict(views or {})
     want = {k: views.get(k, True) for k in ("overview", "model", "kernel", "op", "dist",
                                             "memcpy")}
@@ -159,6 +180,8 @@ def summarize(events, views=None, steps=1, memory=False, top=25):
                 a[0] += 1
                 a[1] += e.cpu_time_total / 1e3
                 a[2] += _dev_time(e) / 1e3
+        for k, ms in (device_phase_ms or {}).items():
+            agg.setdefault(k, [0, 0.0, 0.0])[2] = ms
         rows = []
         order = [p for p in PHASES if p in agg] + sorted(k for k in agg if k not in PHASES)
         for k in order:
@@ -169,7 +192,7 @@ def summarize(events, views=None, steps=1, memory=False, top=25):
     if want["kernel"]:
         agg = {}
         for e in kernels:
-            a = agg.setdefault(e.name, [0, 0.0])
+            a = agg.setdefault(_short(e.name), [0, 0.0])
             a[0] += 1
             a[1] += (e.time_range.end - e.time_range.start) / 1e3
         tot = sum(v[1] for v in agg.values()) or 1.0
@@ -262,11 +285,33 @@ class Profiler:
             with_stack=False)
 
     def start(self):
-        _PHASES["profiling"] = True
+        self._step = 0
         self.prof.start()
+        self._arm()
+
+    def _arm(self):
+        # phases are recorded only inside the active [start, end) window
+        active = self.start_step <= self._step < self.end_step
+        _PHASES["profiling"] = active
+        if not active:
+            return
+        if self._step == self.start_step:
+            _PHASES["marks"] = []
 
     def step(self):
         self.prof.step()
+        self._step += 1
+        self._arm()
+
+    def _device_phase_ms(self):
+        if not torch.cuda.is_available():
+            return {}
+        torch.cuda.synchronize()
+        out = {}
+        for name, a, b in _PHASES["marks"]:
+            out[name] = out.get(name, 0.0) + a.elapsed_time(b)
+        _PHASES["marks"] = []
+        return out
 
     def stop(self):
         self.prof.stop()
@@ -274,7 +319,7 @@ class Profiler:
         try:
             self.text = summarize(self.prof.events(), self.views,
                                   steps=max(1, self.end_step - self.start_step),
-                                  memory=self.memory)
+                                  memory=self.memory, device_phase_ms=self._device_phase_ms())
             logger.info(self.text)
             with open(os.path.join(self.log_dir, "summary_rank%d.txt" % self.rank), "w") as f:
                 f.write(self.text + "\n")
