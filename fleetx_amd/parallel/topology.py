@@ -273,7 +273,10 @@ def init_distributed(backend=None, timeout_s=1800):
             torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
         return dist.is_initialized()
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # FLEETX_DIST_BACKEND=gloo rehearses multi-rank GPU code paths with
+        # several ranks sharing one device (RCCL refuses duplicate GPUs)
+        backend = os.environ.get("FLEETX_DIST_BACKEND") or \
+            ("nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
     kw = {}
