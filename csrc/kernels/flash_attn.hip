@@ -30,6 +30,7 @@ typedef short v4s __attribute__((ext_vector_type(4)));
 namespace {
 
 constexpr float LOG2E = 1.4426950408889634f;
+#define FA_DKDV_QT 32  // query rows per dK/dV tile
 constexpr float LN2 = 0.6931471805599453f;
 
 template <int D>
@@ -516,22 +517,28 @@ __device__ __forceinline__ uint32_t dpp_swap1(uint32_t v) {
 }
 
 // ============================================================================
-// backward dK/dV: WG = 4 waves x 32 keys = 128 keys; loop over 64-query tiles
+// backward dK/dV: WG = 4 waves x 32 keys = 128 keys; loop over 32-query tiles
 //   S = Q.K^T, dP = dO.V^T (keys on lanes, queries in registers)
 //   dV^T += dO^T.(P o Z),  dK^T += Q^T.dS
 // The Q / dO tiles and their lse / delta row constants are double-buffered:
 // tile i+1 streams into the second LDS buffer (global_load_lds) while tile i
 // computes, one vmcnt drain + barrier per tile.
+// Occupancy: the dK and dV accumulators (128 VGPRs) plus K fragments (32)
+// stay in registers; this WG's V rows (128 x D) live in LDS instead of 32
+// more VGPRs, and the query tile is 32 rows, so the kernel fits 256 VGPRs
+// without spills -> 2 waves per SIMD (2 WGs per CU, 65 KB LDS each) instead
+// of 1 wave per SIMD with every LDS / exp latency exposed.
 // Dropout: lanes 2j, 2j+1 hold keys 2j, 2j+1 = the two 16-bit halves of ONE
 // hash per query row, so each lane hashes every other query row and the
 // pair trades results through DPP (one hash per two elements, as fwd / dQ).
 // ============================================================================
 template <int D, bool CAUSAL, bool DROP, bool KB>
-__global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnParams P) {
+__global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int QT = 64, TB = QT * D * 2;
-  // one buffer: [Q tile][dO tile][lse2 64 floats][delta 64 floats]
+  constexpr int QT = FA_DKDV_QT, TB = QT * D * 2;
+  // one buffer: [Q tile][dO tile][lse2 QT floats][delta QT floats]; then V rows
   constexpr int BUF = 2 * TB + 2 * QT * 4;
+  char* vs = smem + 2 * BUF;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
   const int nk = (P.Sk + 127) / 128;
   const int nblk = nk * P.B * P.H;
@@ -550,17 +557,16 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnParams P) {
   const int ki = wk0 + (lane & 31);
   const bool kvalid = ki < kv_len;
   const float kb2 = KB ? P.kbias[(long)b * P.kb_b + ki] * LOG2E : 0.f;
-  bf16x8 kf[D / 16], vf[D / 16];
+  bf16x8 kf[D / 16];
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) {
-    if (ki < P.Sk) {
+    if (ki < P.Sk)
       kf[s] = *reinterpret_cast<const bf16x8*>(kp + (long)ki * P.sk_s + 16 * s + 8 * h);
-      vf[s] = *reinterpret_cast<const bf16x8*>(vp + (long)ki * P.sv_s + 16 * s + 8 * h);
-    } else {
+    else
       kf[s] = __builtin_bit_cast(bf16x8, (short8){0, 0, 0, 0, 0, 0, 0, 0});
-      vf[s] = kf[s];
-    }
   }
+  // V rows of this WG's 128 keys -> LDS (rows past Sk clamp; those keys are masked)
+  Glds<D, 128>::load(vp, P.sv_s, kblock * 128, P.Sk, vs, w, lane);
   floatx16 dkacc[D / 32], dvacc[D / 32];
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt)
@@ -616,18 +622,11 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnParams P) {
     const float* dl_s = lse_s + QT;
     if (!(CAUSAL && qb + QT - 1 < wk0)) {  // else: whole tile above this wave's keys
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      for (int t = 0; t < QT / 32; ++t) {
         const int q0 = qb + 32 * t;
         if (CAUSAL && q0 + 31 < wk0) continue;
-        floatx16 sacc, dpacc;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sacc[i] = dpacc[i] = 0.f;
-#pragma unroll
-        for (int s = 0; s < D / 16; ++s) {
-          sacc = mfma(row_frag<D>(qt, 32 * t + (lane & 31), s, h), kf[s], sacc);
-          dpacc = mfma(row_frag<D>(gt, 32 * t + (lane & 31), s, h), vf[s], dpacc);
-        }
-        float zs[16];
+        uint32_t keep = 0u;  // bit i: element i survives dropout (one VGPR, not 16);
+        // hashed before the MFMAs so its temporaries die before the accumulators live
         if (DROP) {
           // registers i, i+1 (i even) are query rows q, q+1 of this lane's key
 #pragma unroll
@@ -640,28 +639,34 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnParams P) {
             const uint32_t hq1 = (lane & 1) ? mine : other;  // hash of row q + 1
             const uint32_t r0 = (lane & 1) ? (hq >> 16) : (hq & 0xffffu);
             const uint32_t r1 = (lane & 1) ? (hq1 >> 16) : (hq1 & 0xffffu);
-            zs[i] = r0 >= P.thr ? P.drop_scale : 0.f;
-            zs[i + 1] = r1 >= P.thr ? P.drop_scale : 0.f;
+            keep |= (r0 >= P.thr ? 1u : 0u) << i;
+            keep |= (r1 >= P.thr ? 1u : 0u) << (i + 1);
           }
         }
-        floatx16 pd;  // dropped probabilities (for dV)
+        floatx16 sacc, dpacc;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int ql_ = 32 * t + crow(i, h);
-          const int q = qb + ql_;
-          float p = fexp2(sacc[i] * sl2 + kb2 - lse_s[ql_]);
-          if ((CAUSAL && ki > q) || !kvalid || q >= P.Sq) p = 0.f;
-          const float z = DROP ? zs[i] : 1.f;
-          pd[i] = p * z;
-          sacc[i] = p * (dpacc[i] * z - dl_s[ql_]);  // dS
+        for (int i = 0; i < 16; ++i) sacc[i] = dpacc[i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s) {
+          sacc = mfma(row_frag<D>(qt, 32 * t + (lane & 31), s, h), kf[s], sacc);
+          dpacc = mfma(row_frag<D>(gt, 32 * t + (lane & 31), s, h),
+                       row_frag<D>(vs, 32 * w + (lane & 31), s, h), dpacc);
         }
+        // P o Z (for dV) and dS (for dK) straight to bf16, one 8-row half at a
+        // time: no fp32 copies of the tile stay live across the MFMAs
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
           bf16x8 pf, df;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            pf[j] = (__bf16)pd[8 * ss + j];
-            df[j] = (__bf16)sacc[8 * ss + j];
+            const int i = 8 * ss + j;
+            const int ql_ = 32 * t + crow(i, h);
+            const int q = qb + ql_;
+            float p = fexp2(sacc[i] * sl2 + kb2 - lse_s[ql_]);
+            if ((CAUSAL && ki > q) || !kvalid || q >= P.Sq) p = 0.f;
+            const float z = DROP ? (((keep >> i) & 1u) ? P.drop_scale : 0.f) : 1.f;
+            pf[j] = (__bf16)(p * z);
+            df[j] = (__bf16)(p * (dpacc[i] * z - dl_s[ql_]));  // dS
           }
           const int qbase = 32 * t + 16 * ss + 4 * h;
 #pragma unroll
@@ -812,7 +817,8 @@ extern "C" int fx_flash_bwd(const void* q, const void* k, const void* v, const v
   }
   {
     const int nk = (Sk + 127) / 128;
-    const size_t smem = 2 * (2 * 64 * D * 2 + 2 * 64 * 4);  // double-buffered Q/dO tiles
+    // double-buffered Q/dO tiles + row constants, then the WG's V rows
+    const size_t smem = 2 * (2 * FA_DKDV_QT * D * 2 + 2 * FA_DKDV_QT * 4) + 128 * D * 2;
     FA_DISPATCH(fa_bwd_dkdv_kernel, D, causal, p > 0.f, kbias != nullptr, nk * B * H, smem, st,
                 P);
   }
