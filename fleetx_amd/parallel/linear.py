@@ -34,6 +34,21 @@ def _mm_out_supported():
 
 
 _WGRAD_TN = os.environ.get("FLEETX_WGRAD_TN", "1") == "1"
+_DGRAD_TN = os.environ.get("FLEETX_DGRAD_TN", "1") == "1"
+
+
+def dgrad(dy, w):
+    """``dy @ w`` (data gradient of ``F.linear(x, w)``).  On GPU the weight is
+    first transposed (LDS-tiled HIP transpose, ~2 B/elt each way) so the GEMM
+    runs as ``F.linear(dy, w^T)`` -- the "TN" layout hipBLASLt's tuned kernels
+    cover (~1.5 vs ~1.3 PFLOP/s for the "NN" call on the GPT-3 6.7B shapes;
+    ``tools/bench_gemm.py``).  ``FLEETX_DGRAD_TN=0`` keeps the direct call."""
+    if _DGRAD_TN and dy.is_cuda and dy.dtype in (torch.bfloat16, torch.float16) \
+            and w.dtype == dy.dtype and w.dim() == 2 and w.shape[0] % 8 == 0 \
+            and w.shape[1] % 8 == 0 and dy.numel() // dy.shape[-1] >= 1024:
+        from ..ops.elementwise import transpose2d
+        return F.linear(dy, transpose2d(w))
+    return torch.matmul(dy, w)
 
 
 def _fused(p):
@@ -128,7 +143,7 @@ class _FusedWgradLinear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        dx = torch.matmul(dy, w)
+        dx = dgrad(dy, w)
         dy2 = dy.reshape(-1, dy.shape[-1])
         x2 = x.reshape(-1, x.shape[-1])
         db = accumulate_wgrad(w, dy2, x2, ctx.bias)
@@ -175,7 +190,7 @@ class _ColumnTPLinear(torch.autograd.Function):
     def backward(ctx, dy):
         import torch.distributed as dist
         x, w = ctx.saved_tensors
-        dx = torch.matmul(dy, w)
+        dx = dgrad(dy, w)
         work = dist.all_reduce(dx, group=ctx.group.group, async_op=True)
         dy2 = dy.reshape(-1, dy.shape[-1])
         dw = _wgrad(w, dy2, x.reshape(-1, x.shape[-1]))
@@ -212,7 +227,7 @@ class _RowTPLinear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        dx = torch.matmul(dy, w)
+        dx = dgrad(dy, w)
         dy2 = dy.reshape(-1, dy.shape[-1])
         dw = _wgrad(w, dy2, x.reshape(-1, x.shape[-1]))
         return dx, dw, None, None

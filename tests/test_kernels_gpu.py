@@ -683,3 +683,14 @@ def test_profiler_kernel_view_shows_hip_kernels(tmp_path):
     model = text.split("Model Summary")[1].split("Kernel Summary")[0]
     fwd = [l for l in model.splitlines() if l.startswith("Forward")][0]
     assert float(fwd.split("|")[3]) > 0.0, model  # device time attributed to the phase
+
+
+def test_tn_dgrad_matches_matmul():
+    from fleetx_amd.parallel import linear as L
+    dy = torch.randn(4, 512, 384, device="cuda").to(torch.bfloat16)
+    w = torch.randn(384, 1024, device="cuda").to(torch.bfloat16)
+    ref = dy.float() @ w.float()
+    out = L.dgrad(dy, w)
+    assert out.shape == (4, 512, 1024)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-1)
+    assert torch.equal(out, L.F.linear(dy, w.t().contiguous()))
