@@ -42,10 +42,14 @@ def dgrad(dy, w):
     first transposed (LDS-tiled HIP transpose, ~2 B/elt each way) so the GEMM
     runs as ``F.linear(dy, w^T)`` -- the "TN" layout hipBLASLt's tuned kernels
     cover (~1.5 vs ~1.3 PFLOP/s for the "NN" call on the GPT-3 6.7B shapes;
-    ``tools/bench_gemm.py``).  ``FLEETX_DGRAD_TN=0`` keeps the direct call."""
+    ``tools/bench_gemm.py``).  ``FLEETX_DGRAD_TN=0`` keeps the direct call.
+
+    The transpose costs ~4 B per weight element at ~4.5 TB/s while the GEMM
+    saves ~13 % of 2*M FLOPs per element at ~1.4 PFLOP/s: it pays off from
+    M ~ 4.5k rows, so smaller micro-batches (pipeline schedules) keep NN."""
     if _DGRAD_TN and dy.is_cuda and dy.dtype in (torch.bfloat16, torch.float16) \
             and w.dtype == dy.dtype and w.dim() == 2 and w.shape[0] % 8 == 0 \
-            and w.shape[1] % 8 == 0 and dy.numel() // dy.shape[-1] >= 1024:
+            and w.shape[1] % 8 == 0 and dy.numel() // dy.shape[-1] >= 6144:
         from ..ops.elementwise import transpose2d
         return F.linear(dy, transpose2d(w))
     return torch.matmul(dy, w)
