@@ -64,6 +64,9 @@ int fx_sample(int, const void*, long, int, int, float, int, float, const float*,
               float*, hipStream_t);
 int fx_decode_attn(const void*, const void*, const void*, void*, const int*, int, int, int, int,
                    int, long, long, long, long, long, long, float, hipStream_t);
+int fx_softmax_fwd(int, int, const void*, const void*, void*, long, int, int, long, float, int,
+                   hipStream_t);
+int fx_softmax_bwd(int, const void*, const void*, void*, long, int, int, float, int, hipStream_t);
 }
 
 #define P(x) reinterpret_cast<void*>(x)
@@ -213,5 +216,14 @@ PYBIND11_MODULE(_kernels, m) {
                           long sob, float scale, ptr st) {
     return fx_decode_attn(CP(q), CP(kc), CP(vc), P(out), reinterpret_cast<const int*>(lens), B, H,
                           D, maxlen, nsplit, sqb, sqh, skb, sks, skh, sob, scale, S(st));
+  });
+  m.def("softmax_fwd", [](int dt, int mdt, ptr x, ptr mask, ptr y, long rows, int Sq, int Sk,
+                          long mask_div, float scale, int causal, ptr st) {
+    return fx_softmax_fwd(dt, mdt, CP(x), CP(mask), P(y), rows, Sq, Sk, mask_div, scale, causal,
+                          S(st));
+  });
+  m.def("softmax_bwd", [](int dt, ptr y, ptr dy, ptr dx, long rows, int Sq, int Sk, float scale,
+                          int causal, ptr st) {
+    return fx_softmax_bwd(dt, CP(y), CP(dy), P(dx), rows, Sq, Sk, scale, causal, S(st));
   });
 }

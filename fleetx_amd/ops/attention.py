@@ -141,6 +141,33 @@ def _padded_bias(key_bias, B, Sk, device):
     return kb
 
 
+def _unfused_attention(q, k, v, causal, dropout_p, key, scale, kv_lens, key_bias):
+    """Materialised-scores path (reference ``core_attn``, ``single_model.py:189-213``)
+    for head dims the flash tiles do not cover: hipBLASLt QK^T / PV GEMMs in
+    the model dtype around the fused HIP softmax (``ops/softmax.py``);
+    padding keys / key bias enter as one additive ``[B, 1, 1|Sq, Sk]`` mask."""
+    from .softmax import fused_softmax
+    B, Sq, H, D = q.shape
+    Sk = k.shape[1]
+    qh, kh, vh = (t.permute(0, 2, 1, 3) for t in (q, k, v))
+    s = torch.matmul(qh, kh.transpose(-1, -2))
+    mask = None
+    if key_bias is not None or kv_lens is not None:
+        mask = torch.zeros(B, 1, 1, Sk, dtype=torch.float32, device=q.device)
+        if key_bias is not None:
+            mask = mask + key_bias.float().view(B, 1, 1, Sk)
+        if kv_lens is not None:
+            pad = torch.arange(Sk, device=q.device).view(1, 1, 1, Sk) >= \
+                kv_lens.to(q.device).view(B, 1, 1, 1)
+            mask = mask.masked_fill(pad, float("-inf"))
+        mask = mask.expand(B, 1, Sq, Sk)
+    p = fused_softmax(s, mask, causal, scale)
+    if dropout_p > 0.0:
+        keep = _rng.attention_keep_mask(B * H, Sq, Sk, dropout_p, key, q.device).view(B, H, Sq, Sk)
+        p = torch.where(keep, p * (1.0 / (1.0 - dropout_p)), torch.zeros_like(p))
+    return torch.matmul(p, vh).permute(0, 2, 1, 3)
+
+
 def _padded_dim(d):
     return 64 if d <= 64 else 128
 
@@ -164,8 +191,8 @@ def flash_attention(q, k, v, causal=True, dropout_p=0.0, key=0, scale=None, kv_l
             if not _WARNED.get(D):
                 _WARNED[D] = True
                 import warnings
-                warnings.warn("head_dim %d > 128: attention falls back to unfused math" % D)
-            return attention_reference(q, k, v, causal, dropout_p, key, scale, kv_lens, key_bias)
+                warnings.warn("head_dim %d > 128: attention runs unfused (GEMM + HIP softmax)" % D)
+            return _unfused_attention(q, k, v, causal, dropout_p, key, scale, kv_lens, key_bias)
         P = _padded_dim(D) - D
         pad = lambda t: torch.nn.functional.pad(t, (0, P))  # noqa: E731
         out = _FlashAttn.apply(pad(q), pad(k), pad(v), None, causal, float(dropout_p), key,

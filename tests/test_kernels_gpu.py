@@ -694,3 +694,61 @@ def test_tn_dgrad_matches_matmul():
     assert out.shape == (16, 512, 1024)
     torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-1)
     assert torch.equal(out, L.F.linear(dy, w.t().contiguous()))
+
+
+# ---------------------------------------------------------------- fused softmax (K04)
+@pytest.mark.parametrize("Sk", [256, 1024, 4096, 200, 6000])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+def test_softmax_mask_fuse_upper_triangle(Sk, dtype):
+    from fleetx_amd.ops.softmax import softmax_mask_fuse_upper_triangle
+    B, H = 2, 3
+    x = (3 * torch.randn(B, H, Sk, Sk, device=DEV)).to(dtype).requires_grad_()
+    y = softmax_mask_fuse_upper_triangle(x, scale=0.5)
+    xr = x.detach().float().requires_grad_()
+    tri = torch.triu(torch.ones(Sk, Sk, dtype=torch.bool, device=DEV), 1)
+    yr = torch.softmax((xr * 0.5).masked_fill(tri, float("-inf")), -1)
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert _rel(y, yr) < tol
+    assert (y.float().masked_select(tri.expand_as(y)) == 0).all()
+    dy = torch.randn_like(yr)
+    y.backward(dy.to(dtype))
+    yr.backward(dy)
+    assert _rel(x.grad, xr.grad) < (1e-4 if dtype == torch.float32 else 3e-2)
+
+
+@pytest.mark.parametrize("mshape", ["b1", "11", "bh"])
+@pytest.mark.parametrize("Sk", [512, 2048, 77])
+def test_softmax_mask_fuse(mshape, Sk):
+    from fleetx_amd.ops.softmax import softmax_mask_fuse
+    B, H, Sq = 2, 4, 64
+    x = torch.randn(B, H, Sq, Sk, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    lead = {"b1": (B, 1), "11": (1, 1), "bh": (B, H)}[mshape]
+    mask = torch.where(torch.rand(*lead, Sq, Sk, device=DEV) < 0.2, -1e4, 0.0)
+    mask[..., 0, :] = float("-inf")  # a fully masked row -> zeros
+    y = softmax_mask_fuse(x, mask)
+    xr = x.detach().float().requires_grad_()
+    yr = torch.nan_to_num(torch.softmax(xr + mask, -1), nan=0.0)
+    assert _rel(y, yr) < 2e-2
+    assert (y[..., 0, :] == 0).all()
+    dy = torch.randn_like(yr)
+    y.backward(dy.bfloat16())
+    yr.backward(dy)
+    # torch's softmax backward of an all -inf row is NaN; the kernel gives 0
+    assert (x.grad[..., 0, :] == 0).all()
+    assert _rel(x.grad, torch.nan_to_num(xr.grad, nan=0.0)) < 3e-2
+
+
+def test_unfused_attention_wide_heads():
+    """head_dim > 128 runs GEMM + HIP softmax; compare with the fp32 oracle."""
+    import warnings
+    from fleetx_amd.ops.attention import attention_reference, flash_attention
+    B, S, H, D = 2, 256, 2, 160
+    q, k, v = (torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+               for _ in range(3))
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        o = flash_attention(q, k, v, causal=True)
+    ref = attention_reference(q.detach().float(), k.detach().float(), v.detach().float(), True)
+    assert _rel(o, ref) < 2e-2
+    o.float().sum().backward()
+    assert q.grad is not None and torch.isfinite(q.grad.float()).all()
