@@ -64,6 +64,8 @@ int fx_sample(int, const void*, long, int, int, float, int, float, const float*,
               float*, hipStream_t);
 int fx_decode_attn(const void*, const void*, const void*, void*, const int*, int, int, int, int,
                    int, long, long, long, long, long, long, float, hipStream_t);
+void fx_embedding_bwd_sorted(int, const int64_t*, const int64_t*, const void*, float*, int, int,
+                             long, long, hipStream_t);
 int fx_softmax_fwd(int, int, const void*, const void*, void*, long, int, int, long, float, int,
                    hipStream_t);
 int fx_softmax_bwd(int, const void*, const void*, void*, long, int, int, float, int, hipStream_t);
@@ -157,6 +159,12 @@ PYBIND11_MODULE(_kernels, m) {
                             long vsize, ptr st) {
     fx_embedding_bwd(dt, reinterpret_cast<const int64_t*>(ids), CP(dout), F(dW), ntok, h, vstart,
                      vsize, S(st));
+  });
+  m.def("embedding_bwd_sorted", [](int dt, ptr sid, ptr perm, ptr dout, ptr dW, int ntok, int h,
+                                   long vstart, long vsize, ptr st) {
+    fx_embedding_bwd_sorted(dt, reinterpret_cast<const int64_t*>(sid),
+                            reinterpret_cast<const int64_t*>(perm), CP(dout), F(dW), ntok, h,
+                            vstart, vsize, S(st));
   });
   m.def("flash_fwd", [](ptr q, ptr k, ptr v, ptr out, ptr lse, std::vector<long> qs,
                         std::vector<long> ks, std::vector<long> vs, std::vector<long> os,

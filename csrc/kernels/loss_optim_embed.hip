@@ -258,6 +258,32 @@ __global__ __launch_bounds__(256) void embedding_bwd_kernel(const int64_t* __res
   for (int c = lane; c < h; c += 64) atomicAdd(dst + c, Elt<T>::to_f(src[c]));
 }
 
+// Deterministic variant (Global.deterministic): ids pre-sorted (stable) with
+// their token permutation; the wave at the head of each equal-id segment sums
+// that segment's rows in token order and does a plain read-add-write, so the
+// fp32 result is bitwise reproducible run to run (no atomics ordering).
+template <typename T>
+__global__ __launch_bounds__(256) void embedding_bwd_sorted_kernel(
+    const int64_t* __restrict__ sid, const int64_t* __restrict__ perm,
+    const uint16_t* __restrict__ dout, float* __restrict__ dW, int ntok, int h, long vstart,
+    long vsize) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= ntok) return;
+  const long id = sid[i];
+  if (i > 0 && sid[i - 1] == id) return;  // not a segment head
+  const long row = id - vstart;
+  if (row < 0 || row >= vsize) return;
+  int end = i + 1;
+  while (end < ntok && sid[end] == id) ++end;
+  float* dst = dW + (size_t)row * h;
+  for (int c = lane; c < h; c += 64) {
+    float acc = dst[c];
+    for (int j = i; j < end; ++j) acc += Elt<T>::to_f(dout[(size_t)perm[j] * h + c]);
+    dst[c] = acc;
+  }
+}
+
 inline int grid_n(long n, int per = 256) {
   long g = (n + per - 1) / per;
   if (g > 4096) g = 4096;
@@ -330,4 +356,11 @@ extern "C" void fx_embedding_bwd(int dtype, const int64_t* ids, const void* dout
                                  int ntok, int h, long vstart, long vsize, hipStream_t st) {
   FX_DISPATCH_T(dtype, embedding_bwd_kernel<T><<<(ntok + 3) / 4, 256, 0, st>>>(
                            ids, (const uint16_t*)dout, dW, ntok, h, vstart, vsize));
+}
+
+extern "C" void fx_embedding_bwd_sorted(int dtype, const int64_t* sid, const int64_t* perm,
+                                        const void* dout, float* dW, int ntok, int h, long vstart,
+                                        long vsize, hipStream_t st) {
+  FX_DISPATCH_T(dtype, embedding_bwd_sorted_kernel<T><<<(ntok + 3) / 4, 256, 0, st>>>(
+                           sid, perm, (const uint16_t*)dout, dW, ntok, h, vstart, vsize));
 }

@@ -76,7 +76,9 @@ py::array build_sample_idx(const py::array_t<int32_t>& sizes_, const py::array_t
   auto sizes = sizes_.unchecked<1>();
   auto doc_idx = doc_idx_.unchecked<1>();
   const int64_t num_samples = (num_epochs * tokens_per_epoch - 1) / seq_length;
+  const int64_t ndoc_idx = doc_idx.shape(0), nsizes = sizes.shape(0);
   auto* out = new std::vector<int32_t>(2 * (num_samples + 1));
+  bool overrun = false;  // doc_idx holds fewer tokens than num_epochs * tokens_per_epoch
   {
     py::gil_scoped_release nogil;
     int32_t* o = out->data();
@@ -84,10 +86,14 @@ py::array build_sample_idx(const py::array_t<int32_t>& sizes_, const py::array_t
     int32_t offset = 0;  // token offset inside the current document
     o[0] = 0;
     o[1] = 0;
-    for (int64_t s = 1; s <= num_samples; ++s) {
+    for (int64_t s = 1; s <= num_samples && !overrun; ++s) {
       // a sample spans seq_length + 1 tokens; consecutive samples share one
       int32_t need = seq_length + 1;
       for (;;) {
+        if (d >= ndoc_idx || doc_idx[d] < 0 || doc_idx[d] >= nsizes) {
+          overrun = true;
+          break;
+        }
         const int32_t avail = sizes[doc_idx[d]] - offset;
         if (avail >= need) {
           offset += need - 1;
@@ -100,6 +106,12 @@ py::array build_sample_idx(const py::array_t<int32_t>& sizes_, const py::array_t
       o[2 * s] = static_cast<int32_t>(d);
       o[2 * s + 1] = offset;
     }
+  }
+  if (overrun) {
+    delete out;
+    throw std::invalid_argument(
+        "build_sample_idx: doc_idx/sizes hold fewer tokens than num_epochs * tokens_per_epoch "
+        "(or a doc id is out of range)");
   }
   return to_numpy(out, num_samples + 1, 2);
 }

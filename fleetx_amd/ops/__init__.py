@@ -6,5 +6,7 @@ from .attention import (flash_attention, flash_attention_qkvpacked, attention_re
 from .loss_embed import softmax_cross_entropy, embedding  # noqa: F401
 from .quant import fake_quant  # noqa: F401
 from .sampling import fused_sample  # noqa: F401
+from .softmax import (fused_softmax, softmax_mask_fuse,  # noqa: F401
+                      softmax_mask_fuse_upper_triangle)
 from . import _lib  # noqa: F401
 from .groupnorm import group_norm_silu, GroupNormSiLU  # noqa: F401,E402

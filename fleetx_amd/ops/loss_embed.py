@@ -8,6 +8,8 @@ tensor-parallel combine is two RCCL all-reduces of [tokens] fp32 vectors
 (max, then the packed [sum, target] pair).  Backward overwrites the logits in
 place with ``(softmax - onehot) * g``.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -83,6 +85,21 @@ def softmax_cross_entropy(logits, labels, group=None, vocab_start=0, ignore_inde
     return _SoftmaxCE.apply(logits, labels, group, vocab_start, ignore_index, inplace_backward)
 
 
+def deterministic():
+    """``Global.deterministic`` / ``FLEETX_DETERMINISTIC=1``: reproducible
+    reductions (no fp32 atomics in the embedding backward)."""
+    return os.environ.get("FLEETX_DETERMINISTIC", "0") == "1"
+
+
+def _embedding_bwd(k, dc, ids, d, dw32, ntok, h, vstart, vsize, st):
+    if deterministic():
+        sid, perm = torch.sort(ids.reshape(-1), stable=True)
+        k.embedding_bwd_sorted(dc, sid.data_ptr(), perm.data_ptr(), d.data_ptr(), dw32.data_ptr(),
+                               ntok, h, vstart, vsize, st)
+        return
+    k.embedding_bwd(dc, ids.data_ptr(), d.data_ptr(), dw32.data_ptr(), ntok, h, vstart, vsize, st)
+
+
 def _grad_target(p, shape, device):
     """fp32 buffer the scatter-add kernel accumulates into: the parameter's
     flat-buffer ``main_grad`` when it takes fused gradients (no bf16 round
@@ -144,13 +161,11 @@ class _Embedding(torch.autograd.Function):
             st = _lib.stream()
             wp, pp = ctx.params
             dw32, fused = _grad_target(wp, (ctx.vsize, h), d.device)
-            k.embedding_bwd(dc, ids_c.data_ptr(), d.data_ptr(), dw32.data_ptr(), ntok, h,
-                            int(ctx.vocab_start), ctx.vsize, st)
+            _embedding_bwd(k, dc, ids_c, d, dw32, ntok, h, int(ctx.vocab_start), ctx.vsize, st)
             dw = _grad_finish(wp, dw32, fused, ctx.wdtype)
             if ctx.has_pos:
                 dp32, fused = _grad_target(pp, (ctx.pos_rows, h), d.device)
-                k.embedding_bwd(dc, pos_c.data_ptr(), d.data_ptr(), dp32.data_ptr(), ntok, h, 0,
-                                ctx.pos_rows, st)
+                _embedding_bwd(k, dc, pos_c, d, dp32, ntok, h, 0, ctx.pos_rows, st)
                 dpos = _grad_finish(pp, dp32, fused, ctx.wdtype)
         else:
             wp, pp = ctx.params

@@ -27,6 +27,7 @@ def get_world_size():
 
 def init_dist_env(config, backend=None):
     """Create the process group and the hybrid topology from ``Distributed``."""
+    set_debug_modes(config)
     d = config.Distributed
     # collective debugging (SURVEY §5.2, new vs. the reference): "detail" wraps every
     # process group so each collective first cross-checks op / shape / dtype
@@ -64,6 +65,29 @@ def set_seed(seed):
                                data_rank=data_rank)
     # parameter-init seed for mp-sharded weights (reference env.py:67)
     return s
+
+
+def set_debug_modes(config):
+    """Debug / reproducibility switches (new vs. the reference):
+
+    * ``Global.deterministic``: ``torch.use_deterministic_algorithms`` plus
+      this framework's deterministic kernels (sorted-segment embedding
+      backward instead of fp32 atomics) -- bitwise-reproducible steps for
+      golden tests;
+    * ``Global.kernel_sync``: synchronise after every HIP kernel launch of
+      ours (``FLEETX_KERNEL_SYNC``) and serialise HIP launches
+      (``AMD_SERIALIZE_KERNEL=3``), so a faulting kernel is reported at its
+      own launch.  Both are read at process start, so they are set before
+      the first kernel is loaded."""
+    g = config.get("Global", {}) or {}
+    if g.get("deterministic", False):
+        os.environ["FLEETX_DETERMINISTIC"] = "1"
+        torch.use_deterministic_algorithms(True, warn_only=True)
+    if g.get("kernel_sync", False):
+        os.environ.setdefault("AMD_SERIALIZE_KERNEL", "3")
+        os.environ["FLEETX_KERNEL_SYNC"] = "1"
+        from ..ops import _lib
+        _lib.DEBUG_SYNC = True
 
 
 def device():

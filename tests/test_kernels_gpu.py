@@ -752,3 +752,24 @@ def test_unfused_attention_wide_heads():
     assert _rel(o, ref) < 2e-2
     o.float().sum().backward()
     assert q.grad is not None and torch.isfinite(q.grad.float()).all()
+
+
+def test_embedding_bwd_deterministic(monkeypatch):
+    """Sorted-segment embedding backward (Global.deterministic) equals the atomic path
+    numerically and is bitwise reproducible."""
+    from fleetx_amd import ops
+    V, h, ntok = 1000, 256, 4096
+    ids = torch.randint(0, 50, (ntok,), device=DEV)  # heavy repeats
+    w = torch.randn(V, h, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    dy = torch.randn(ntok, h, device=DEV, dtype=torch.bfloat16)
+
+    def grad():
+        w.grad = None
+        ops.embedding(ids, w).backward(dy)
+        return w.grad.float().clone()
+    g_atomic = grad()
+    monkeypatch.setenv("FLEETX_DETERMINISTIC", "1")
+    g1, g2 = grad(), grad()
+    assert torch.equal(g1, g2)
+    ref = torch.zeros(V, h, device=DEV).index_add_(0, ids, dy.float())
+    assert _rel(g1, ref) < 1e-2 and _rel(g_atomic, ref) < 1e-2

@@ -31,3 +31,18 @@ def test_mask_row_divisor():
     assert _mask_div(x, torch.empty(2, 4, 8, 8)) == 1
     with pytest.raises(ValueError):
         _mask_div(x, torch.empty(1, 4, 8, 8))
+
+
+def test_debug_modes(monkeypatch):
+    import os
+    from fleetx_amd.utils import env
+    from fleetx_amd.utils.config import AttrDict
+    monkeypatch.delenv("FLEETX_DETERMINISTIC", raising=False)
+    cfg = AttrDict({"Global": AttrDict({"deterministic": True, "kernel_sync": False})})
+    try:
+        env.set_debug_modes(cfg)
+        assert os.environ["FLEETX_DETERMINISTIC"] == "1"
+        assert torch.are_deterministic_algorithms_enabled()
+    finally:
+        torch.use_deterministic_algorithms(False)
+        os.environ.pop("FLEETX_DETERMINISTIC", None)
