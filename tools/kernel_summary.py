@@ -1,6 +1,6 @@
 """Summarise a rocprofv3 kernel trace (``*_kernel_trace.csv`` or
-``*_kernel_stats.csv``) into a short per-kernel table: total ms per step,
-calls, share -- with template noise stripped from the names.
+``*_kernel_stats.csv``, or the rocpd ``*_results.db`` that ROCm 7 writes by
+default) into a short per-kernel table: total ms per step, calls, share -- with template noise stripped from the names.
 
     python tools/kernel_summary.py trace.csv [--steps N] [--top 30] [--md out.md]
         [--window adamw_flat:2:6]
@@ -40,8 +40,23 @@ def _window(rows, spec):
     return [r for r in rows if lo < float(r["Start_Timestamp"]) <= hi]
 
 
+def _rows_from_rocpd(path):
+    """ROCm 7 rocprofv3 writes a rocpd SQLite database (``*_results.db``) by
+    default; its ``kernels`` view has one row per dispatch."""
+    import sqlite3
+    con = sqlite3.connect(path)
+    try:
+        return [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e}
+                for n, s, e in con.execute("select name, start, end from kernels order by start")]
+    finally:
+        con.close()
+
+
 def load(path, window=None):
-    rows = list(csv.DictReader(open(path)))
+    if path.endswith(".db"):
+        rows = _rows_from_rocpd(path)
+    else:
+        rows = list(csv.DictReader(open(path)))
     if window:
         rows = _window(rows, window)
     agg = collections.defaultdict(lambda: [0.0, 0])
