@@ -69,6 +69,9 @@ void fx_embedding_bwd_sorted(int, const int64_t*, const int64_t*, const void*, f
 int fx_softmax_fwd(int, int, const void*, const void*, void*, long, int, int, long, float, int,
                    hipStream_t);
 int fx_softmax_bwd(int, const void*, const void*, void*, long, int, int, float, int, hipStream_t);
+int fx_gemm(int, int, int, int, int, int, int, const void*, long, const void*, long, void*, long,
+            const void*, void*, long, int, hipStream_t);
+void fx_gemm_set_variant(int);
 }
 
 #define P(x) reinterpret_cast<void*>(x)
@@ -230,6 +233,12 @@ PYBIND11_MODULE(_kernels, m) {
     return fx_softmax_fwd(dt, mdt, CP(x), CP(mask), P(y), rows, Sq, Sk, mask_div, scale, causal,
                           S(st));
   });
+  m.def("gemm", [](int dt, int la, int lb, int epi, int M, int N, int K, ptr A, long lda, ptr B,
+                   long ldb, ptr C, long ldc, ptr bias, ptr aux, long ldaux, int beta, ptr st) {
+    return fx_gemm(dt, la, lb, epi, M, N, K, CP(A), lda, CP(B), ldb, P(C), ldc, CP(bias), P(aux),
+                   ldaux, beta, S(st));
+  });
+  m.def("gemm_set_variant", &fx_gemm_set_variant);
   m.def("softmax_bwd", [](int dt, ptr y, ptr dy, ptr dx, long rows, int Sq, int Sk, float scale,
                           int causal, ptr st) {
     return fx_softmax_bwd(dt, CP(y), CP(dy), P(dx), rows, Sq, Sk, scale, causal, S(st));

@@ -10,8 +10,10 @@ residual; final LN; LM head tied to the word embedding; loss
 ``full_attn`` / ``core_attn``.
 
 MI355X mapping:
-* QKV / out-proj / FFN GEMMs: hipBLASLt via ``F.linear`` (bias-free);
-* bias+GeLU, bias+dropout+residual, residual+LN2: HIP epilogue kernels;
+* QKV / out-proj / FFN / LM-head GEMMs: the hand-written MFMA GEMM
+  (``ops.gemm``) in native layouts; FC1 bias+GeLU and FC2's dgrad*gelu' are
+  fused into GEMM epilogues (``parallel.linear.fused_mlp``), the QKV bias too;
+* bias+dropout+residual, residual+LN2: HIP epilogue kernels;
 * attention: the fused flash kernel reading the packed ``[.., heads, 3, d]``
   QKV output in place;
 * embedding gather and vocab-parallel CE: HIP kernels; logits gradient is
@@ -28,6 +30,7 @@ from .... import ops
 from ....parallel import layers as L
 from ....parallel import mappings as M
 from ....parallel import topology as topo
+from ....parallel.linear import fused_mlp
 from ....parallel.recompute import recompute
 from ....parallel.rng import get_rng_state_tracker
 
@@ -165,6 +168,11 @@ class GPTMLP(nn.Module):
                                        std=std, name="layers.%d.mlp.fc2" % idx, dtype=cfg.dtype)
 
     def forward(self, x):
+        if topo.mp_world_size() == 1 and type(self.fc1) is L.ColumnParallelLinear \
+                and type(self.fc2) is L.RowParallelLinear:
+            # one autograd node: FC1 GEMM+bias+GeLU epilogue, FC2 GEMM; backward
+            # fuses gelu' into FC2's data-gradient GEMM (parallel/linear.py)
+            return fused_mlp(x, self.fc1.weight, self.fc1.bias, self.fc2.weight), self.fc2.bias
         y, b = self.fc1(x)
         y = ops.bias_gelu(y, b, approximate=True)
         return self.fc2(y)

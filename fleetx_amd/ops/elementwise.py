@@ -75,6 +75,34 @@ def bias_gelu(x, bias=None, approximate=True):
     return _BiasGelu.apply(x, bias, not approximate)
 
 
+def gelu_plain(h, erf=False):
+    """``gelu(h)`` without autograd (fallback half of the fused FC1 epilogue)."""
+    h = h.contiguous()
+    if h.is_cuda:
+        y = torch.empty_like(h)
+        _lib.kernels().bias_gelu_fwd(_lib.dt_code(h.dtype), int(erf), h.data_ptr(), 0,
+                                     y.data_ptr(), h.numel(), h.shape[-1], _lib.stream())
+        return y
+    return _gelu_ref(h.float(), erf).to(h.dtype)
+
+
+def gelu_grad(dy, h, erf=False):
+    """``dy * gelu'(h)`` without autograd (fallback of the fused dGeLU epilogue)."""
+    dy = dy.contiguous()
+    h = h.contiguous()
+    if dy.is_cuda:
+        k = _lib.kernels()
+        cols = h.shape[-1]
+        rows = h.numel() // cols
+        splits = k.coltile_splits(rows, cols)
+        part = torch.empty(splits, cols, device=h.device, dtype=torch.float32)
+        dx = torch.empty_like(h)
+        k.bias_gelu_bwd(_lib.dt_code(h.dtype), int(erf), dy.data_ptr(), h.data_ptr(), 0,
+                        dx.data_ptr(), part.data_ptr(), rows, cols, splits, _lib.stream())
+        return dx
+    return (dy.float() * _gelu_grad_ref(h.float(), erf)).to(h.dtype)
+
+
 class _BiasDropoutAdd(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, bias, residual, p, key):

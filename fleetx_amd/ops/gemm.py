@@ -1,0 +1,155 @@
+"""Linear-layer GEMMs on the hand-written gfx950 MFMA kernel (csrc/kernels/gemm.hip).
+
+Three entry points cover the three GEMMs of a linear layer ``y = x W^T (+b)``
+with the weight stored ``[out, in]``, each in its NATIVE layout (no transposed
+copies):
+
+* :func:`linear_fwd`   ``y = x W^T (+ b)``, optionally with the tanh/erf GeLU
+  epilogue (returns ``(gelu(h), h)``; ``h`` is the pre-activation kept for the
+  backward pass).  A = x ``[M][K]`` (k-contiguous), B = W ``[N][K]``.
+* :func:`linear_dgrad` ``dx = dy W``, optionally times ``gelu'(h)`` in the
+  epilogue (FC2's data gradient becomes FC1's dH directly).  A = dy
+  ``[M][N]``, B = W read as ``[K=N][n=in]`` (mn-contiguous, hardware
+  transposed LDS reads).
+* :func:`linear_wgrad` ``main_grad (+)= dy^T x`` in fp32 (beta 0/1).  Both
+  operands token-major (mn-contiguous).
+
+Each returns ``None`` when the kernel does not cover the shape (K not a
+multiple of 64, odd extents, non-unit inner strides, fp32 tensors); the
+caller then uses hipBLASLt.  ``FLEETX_GEMM=hip`` routes every covered GEMM
+here, ``blas`` none, ``auto`` (default) the kinds in ``FLEETX_GEMM_AUTO``.
+
+Parity: the reference's ``FusedLinear`` / ``fused_gemm_epilogue``
+(``gpt/dygraph/single_model.py:29,81,375``; ``language_model/utils.py:30-36``).
+"""
+import os
+
+import torch
+
+from . import _lib
+
+LAY_KC, LAY_MC = 0, 1
+EPI_STORE, EPI_BIAS_GELU, EPI_DGELU, EPI_F32, EPI_BIAS_GELU_ERF, EPI_DGELU_ERF = range(6)
+
+_MODE = os.environ.get("FLEETX_GEMM", "auto")
+
+
+def enabled():
+    return _MODE != "blas"
+
+
+def set_mode(mode):
+    """'hip' (default), 'blas' (hipBLASLt everywhere) or 'auto' (per-kind table)."""
+    global _MODE
+    _MODE = mode
+
+
+# GEMM kinds routed to the MFMA kernel under FLEETX_GEMM=auto (kinds where it
+# beats hipBLASLt incl. the transposes hipBLASLt needs; tools/bench_gemm.py)
+AUTO_KINDS = set(k for k in os.environ.get("FLEETX_GEMM_AUTO", "wgrad").split(",") if k)
+
+
+def use(kind, a, b=None):
+    """Whether GEMM ``kind`` ('fwd' | 'dgrad' | 'wgrad') on these operands goes
+    to the MFMA kernel (the kernel itself may still decline the shape)."""
+    if _MODE == "blas" or not a.is_cuda or a.dtype not in (torch.bfloat16, torch.float16):
+        return False
+    if _MODE == "auto":
+        return kind in AUTO_KINDS
+    return True
+
+
+def _ok(*ts):
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda or t.dtype not in (torch.bfloat16, torch.float16) or t.dim() != 2 \
+                or t.stride(1) != 1 or t.data_ptr() % 16 or t.stride(0) % 8:
+            return False
+    return True
+
+
+def _launch(dt, la, lb, epi, M, N, K, A, lda, B, ldb, C, ldc, bias=None, aux=None, ldaux=0,
+            beta=0):
+    return _lib.kernels().gemm(dt, la, lb, epi, M, N, K, A.data_ptr(), lda, B.data_ptr(), ldb,
+                               C.data_ptr(), ldc, _lib.ptr(bias), _lib.ptr(aux), ldaux, int(beta),
+                               _lib.stream())
+
+
+def linear_fwd(x2, w, bias=None, act=None, out=None):
+    """``x2 [M,K] @ w[N,K]^T (+ bias)``; ``act`` in (None, 'gelu', 'gelu_erf').
+    Returns ``y`` or ``(gelu(h), h)``; ``None`` if not covered."""
+    if not enabled() or not _ok(x2, w) or w.dtype != x2.dtype:
+        return None
+    if bias is not None and (bias.dtype != x2.dtype or not bias.is_contiguous()):
+        return None
+    M, K = x2.shape
+    N = w.shape[0]
+    if w.shape[1] != K:
+        raise ValueError("linear_fwd: shape mismatch {} x {}".format(tuple(x2.shape), tuple(w.shape)))
+    y = out if out is not None else torch.empty(M, N, device=x2.device, dtype=x2.dtype)
+    h = None
+    if act is None:
+        epi = EPI_STORE
+    else:
+        epi = EPI_BIAS_GELU if act == "gelu" else EPI_BIAS_GELU_ERF
+        h = torch.empty(M, N, device=x2.device, dtype=x2.dtype)
+    rc = _launch(_lib.dt_code(x2.dtype), LAY_KC, LAY_KC, epi, M, N, K, x2, x2.stride(0), w,
+                 w.stride(0), y, N, bias, h, N)
+    if rc != 0:
+        return None
+    _lib.maybe_sync()
+    return y if act is None else (y, h)
+
+
+def linear_dgrad(dy2, w, act_input=None, act="gelu"):
+    """``dy2 [M,N] @ w [N,K]`` (times ``gelu'(act_input)`` when given)."""
+    if not enabled() or not _ok(dy2, w, act_input) or w.dtype != dy2.dtype:
+        return None
+    M, N = dy2.shape
+    K = w.shape[1]
+    if w.shape[0] != N:
+        raise ValueError("linear_dgrad: shape mismatch")
+    dx = torch.empty(M, K, device=dy2.device, dtype=dy2.dtype)
+    epi = EPI_STORE
+    ld_aux = 0
+    if act_input is not None:
+        epi = EPI_DGELU if act == "gelu" else EPI_DGELU_ERF
+        ld_aux = act_input.stride(0)
+    # C[M, K] = sum_n A[m, n] B[n, k]: A = dy (k-contig over n), B = w stored [n][k]
+    rc = _launch(_lib.dt_code(dy2.dtype), LAY_KC, LAY_MC, epi, M, K, N, dy2, dy2.stride(0), w,
+                 w.stride(0), dx, K, None, act_input, ld_aux)
+    if rc != 0:
+        return None
+    _lib.maybe_sync()
+    return dx
+
+
+def linear_wgrad(dy2, x2, out32, accumulate):
+    """``out32[N,K] (+)= dy2[M,N]^T @ x2[M,K]`` in fp32.  Returns True if done."""
+    if not enabled() or not _ok(dy2, x2) or dy2.dtype != x2.dtype:
+        return False
+    if out32.dtype != torch.float32 or not out32.is_contiguous():
+        return False
+    M, N = dy2.shape
+    K = x2.shape[1]
+    if out32.shape != (N, K):
+        raise ValueError("linear_wgrad: out shape {} != {}".format(tuple(out32.shape), (N, K)))
+    # C[N, K] = sum_m A[n, m] B[m, k]: A = dy stored [m][n], B = x stored [m][k]
+    rc = _launch(_lib.dt_code(dy2.dtype), LAY_MC, LAY_MC, EPI_F32, N, K, M, dy2, dy2.stride(0),
+                 x2, x2.stride(0), out32, K, beta=accumulate)
+    if rc == 0:
+        _lib.maybe_sync()
+    return rc == 0
+
+
+def wgrad_16(dy2, x2):
+    """``dy2^T @ x2`` returned in the 16-bit input dtype (no main_grad)."""
+    if not enabled() or not _ok(dy2, x2) or dy2.dtype != x2.dtype:
+        return None
+    M, N = dy2.shape
+    K = x2.shape[1]
+    out = torch.empty(N, K, device=dy2.device, dtype=dy2.dtype)
+    rc = _launch(_lib.dt_code(dy2.dtype), LAY_MC, LAY_MC, EPI_STORE, N, K, M, dy2, dy2.stride(0),
+                 x2, x2.stride(0), out, K)
+    return out if rc == 0 else None

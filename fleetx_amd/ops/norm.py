@@ -45,6 +45,31 @@ def col_sum(x, cols):
     return out
 
 
+def col_sum_f32(x, dst, accumulate=False):
+    """``dst (+)= x.reshape(-1, cols).sum(0)`` with ``dst`` a contiguous fp32
+    vector (bias gradients straight into ``main_grad``)."""
+    cols = dst.numel()
+    if not x.is_cuda:
+        s = x.reshape(-1, cols).float().sum(0).view_as(dst)
+        if accumulate:
+            dst.add_(s)
+        else:
+            dst.copy_(s)
+        return dst
+    if dst.dtype != torch.float32 or not dst.is_contiguous():
+        raise ValueError("col_sum_f32: dst must be contiguous fp32")
+    x = x.contiguous()
+    k = _lib.kernels()
+    rows = x.numel() // cols
+    splits = k.coltile_splits(rows, cols)
+    p0 = torch.empty(splits, cols, device=x.device, dtype=torch.float32)
+    st = _lib.stream()
+    dc = _lib.dt_code(x.dtype)
+    k.coltile_partial(dc, 1, x.data_ptr(), 0, 0, 0, p0.data_ptr(), 0, rows, cols, splits, st)
+    k.coltile_finalize(dc, p0.data_ptr(), splits, cols, dst.data_ptr(), 0, int(accumulate), st)
+    return dst
+
+
 def _dropout_ref(x, p, key):
     if p <= 0.0:
         return x

@@ -1,5 +1,10 @@
-"""Linear with the weight-gradient GEMM accumulating straight into the fp32
-``main_grad`` buffer.
+"""Linear layers on the hand-written gfx950 GEMM (``ops.gemm``), with the
+weight-gradient GEMM accumulating straight into the fp32 ``main_grad`` buffer.
+
+GEMM routing: every forward / data-gradient / weight-gradient GEMM first tries
+the MFMA kernel in its native operand layout (no transposed copies), with the
+bias, GeLU and GeLU-derivative fused into its epilogue (``fused_mlp``); shapes
+it does not cover (or ``FLEETX_GEMM=blas``) take the hipBLASLt paths below.
 
 Without this, every weight gradient goes hipBLASLt (bf16 dW) -> autograd
 ``.grad`` -> a post-accumulate hook that adds it into the fp32 flat buffer:
@@ -21,6 +26,8 @@ import os
 
 import torch
 import torch.nn.functional as F
+
+from ..ops import gemm as G
 
 _MM_DTYPE_OUT = None
 
@@ -80,6 +87,20 @@ def accumulate_wgrad(weight, dy2, x2, bias=None):
     (returns None), else returned as a tensor for autograd."""
     mg = weight.main_grad
     fresh = getattr(weight, "_fx_fresh", False)
+    if G.use("wgrad", dy2, x2) and G.linear_wgrad(dy2, x2, mg, not fresh):
+        db = None
+        if bias is not None:
+            if _fused(bias):
+                colsum_into(dy2, bias.main_grad, not getattr(bias, "_fx_fresh", False))
+                bias._fx_fresh = False
+                grad_part_done(bias)
+            else:
+                db = torch.empty(bias.shape, device=dy2.device, dtype=torch.float32)
+                colsum_into(dy2, db, False)
+                db = db.to(bias.dtype)
+        weight._fx_fresh = False
+        grad_part_done(weight)
+        return db
     db, colsum = None, None
     if bias is not None:
         if _fused(bias):
@@ -137,17 +158,48 @@ def grad_part_done(p):
         cb()
 
 
+def fwd_gemm(x, weight, bias=None):
+    """``F.linear`` on the MFMA kernel when it covers the shape."""
+    if G.use("fwd", x, weight):
+        x2 = x.reshape(-1, x.shape[-1])
+        y = G.linear_fwd(x2, weight, bias)
+        if y is not None:
+            return y.view(*x.shape[:-1], weight.shape[0])
+    return F.linear(x, weight, bias)
+
+
+def dgrad_gemm(dy, w, act_input=None, act="gelu"):
+    """``dy @ w`` (times ``gelu'(act_input)`` when given) on the MFMA kernel."""
+    if G.use("dgrad", dy, w):
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        ai = None if act_input is None else act_input.reshape(-1, act_input.shape[-1])
+        dx = G.linear_dgrad(dy2, w, act_input=ai, act=act)
+        if dx is not None:
+            return dx.view(*dy.shape[:-1], w.shape[1])
+    dx = dgrad(dy, w)
+    if act_input is not None:
+        from ..ops.elementwise import gelu_grad
+        dx = gelu_grad(dx, act_input, erf=(act != "gelu"))
+    return dx
+
+
+def colsum_into(dy2, dst, accumulate):
+    """``dst (+)= dy2.sum(0)`` in fp32 (HIP column-tile reduction on GPU)."""
+    from ..ops.norm import col_sum_f32
+    col_sum_f32(dy2, dst, accumulate)
+
+
 class _FusedWgradLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.bias = bias
-        return F.linear(x, weight, bias)
+        return fwd_gemm(x, weight, bias)
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        dx = dgrad(dy, w)
+        dx = dgrad_gemm(dy, w)
         dy2 = dy.reshape(-1, dy.shape[-1])
         x2 = x.reshape(-1, x.shape[-1])
         db = accumulate_wgrad(w, dy2, x2, ctx.bias)
@@ -172,6 +224,10 @@ def _wgrad(w, dy2, x2):
     if hasattr(w, "main_grad") and getattr(w, "_fx_fused_wgrad", False):
         accumulate_wgrad(w, dy2, x2)
         return None
+    if G.use("wgrad", dy2, x2):
+        dw = G.wgrad_16(dy2, x2)
+        if dw is not None:
+            return dw
     return torch.mm(dy2.t(), x2).to(w.dtype)
 
 
@@ -188,13 +244,13 @@ class _ColumnTPLinear(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.group = group
         ctx.has_bias = bias is not None
-        return F.linear(x, weight, bias)
+        return fwd_gemm(x, weight, bias)
 
     @staticmethod
     def backward(ctx, dy):
         import torch.distributed as dist
         x, w = ctx.saved_tensors
-        dx = dgrad(dy, w)
+        dx = dgrad_gemm(dy, w)
         work = dist.all_reduce(dx, group=ctx.group.group, async_op=True)
         dy2 = dy.reshape(-1, dy.shape[-1])
         dw = _wgrad(w, dy2, x.reshape(-1, x.shape[-1]))
@@ -222,7 +278,9 @@ class _RowTPLinear(torch.autograd.Function):
         wt = weight.t()
         for i in range(n):
             a, b = bounds[i], bounds[i + 1]
-            torch.mm(x2[a:b], wt, out=y[a:b])
+            if not (G.use("fwd", x2, weight) and G.linear_fwd(x2[a:b], weight, out=y[a:b])
+                    is not None):
+                torch.mm(x2[a:b], wt, out=y[a:b])
             works.append(dist.all_reduce(y[a:b], group=group.group, async_op=True))
         for wk in works:
             wk.wait()
@@ -231,7 +289,7 @@ class _RowTPLinear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        dx = dgrad(dy, w)
+        dx = dgrad_gemm(dy, w)
         dy2 = dy.reshape(-1, dy.shape[-1])
         dw = _wgrad(w, dy2, x.reshape(-1, x.shape[-1]))
         return dx, dw, None, None
@@ -243,3 +301,59 @@ def column_tp_linear(x, weight, bias, group):
 
 def row_tp_linear(x, weight, group, chunks=2):
     return _RowTPLinear.apply(x, weight, group, chunks)
+
+
+# ----------------------------------------------------------------------------
+# Fused MLP (single mp rank): FC1 GEMM + bias + GeLU in one kernel, FC2 GEMM,
+# and in backward FC2's data-gradient GEMM applies gelu'(h) in its epilogue.
+# ----------------------------------------------------------------------------
+class _FusedMLP(torch.autograd.Function):
+    """``y = gelu(x W1^T + b1) W2^T`` (FC2 bias left to the caller's epilogue).
+
+    Saves x, the pre-activation h and the activation a (a feeds FC2's weight
+    gradient); backward: dW2 (+)= dy^T a, dH = (dy W2) * gelu'(h) (one GEMM),
+    db1 = colsum(dH), dW1 (+)= dH^T x, dx = dH W1.  Parity: reference
+    ``GPTMLP`` / fused_feedforward (``gpt/dygraph/single_model.py:375``)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, act):
+        ctx.act = act
+        x2 = x.reshape(-1, x.shape[-1])
+        r = G.linear_fwd(x2, w1, b1, act=act) if G.use("fwd", x2, w1) else None
+        if r is None:
+            from ..ops.elementwise import gelu_plain
+            h = F.linear(x2, w1, b1)
+            a = gelu_plain(h, erf=(act != "gelu"))
+        else:
+            a, h = r
+        y = G.linear_fwd(a, w2) if G.use("fwd", a, w2) else None
+        if y is None:
+            y = F.linear(a, w2)
+        ctx.save_for_backward(x, h, a, w1, b1, w2)
+        return y.view(*x.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, h, a, w1, b1, w2 = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        x2 = x.reshape(-1, x.shape[-1])
+        dw2 = _wgrad(w2, dy2, a)
+        dh = dgrad_gemm(dy2, w2, act_input=h, act=ctx.act)
+        db1 = None
+        if b1 is not None:
+            # the bias takes its fp32 grad directly when it lives in the buffer
+            if hasattr(b1, "main_grad") and getattr(b1, "_fx_grad_ready", None) is not None:
+                colsum_into(dh, b1.main_grad, not getattr(b1, "_fx_fresh", False))
+                b1._fx_fresh = False
+                grad_part_done(b1)
+            else:
+                t = torch.empty(b1.shape, device=dh.device, dtype=torch.float32)
+                colsum_into(dh, t, False)
+                db1 = t.to(b1.dtype)
+        dw1 = _wgrad(w1, dh, x2)
+        dx = dgrad_gemm(dh, w1)
+        return dx.view_as(x), dw1, db1, dw2, None
+
+
+def fused_mlp(x, w1, b1, w2, act="gelu"):
+    return _FusedMLP.apply(x, w1, b1, w2, act)

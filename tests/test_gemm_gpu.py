@@ -1,0 +1,163 @@
+"""Numerics of the hand-written MFMA GEMM (csrc/kernels/gemm.hip) against a
+plain PyTorch fp32 reference of the same op, every layout x epilogue, bf16 and
+fp16, including edge tiles (M, N not multiples of 256) and K-tails."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(256, 256, 64), (512, 768, 1024), (296, 520, 192), (1024, 1000, 320), (64, 256, 128)]
+
+
+def _rel(out, ref):
+    return float((out.float() - ref).abs().max() / ref.abs().max().clamp_min(1e-6))
+
+
+def _gelu(x, erf):
+    return torch.nn.functional.gelu(x, approximate="none" if erf else "tanh")
+
+
+def _gelu_grad(x, erf):
+    x = x.detach().requires_grad_(True)
+    y = _gelu(x, erf)
+    (g,) = torch.autograd.grad(y.sum(), x)
+    return g
+
+
+@pytest.fixture(scope="module")
+def gemm():
+    from fleetx_amd.ops import gemm as G
+    from fleetx_amd.ops import _lib
+    _lib.kernels()
+    G.set_mode("hip")
+    return G
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_fwd_store_bias(gemm, M, N, K, dtype):
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device="cuda", dtype=dtype)
+    w = torch.randn(N, K, device="cuda", dtype=dtype) * 0.05
+    b = torch.randn(N, device="cuda", dtype=dtype)
+    ref = x.float() @ w.float().t()
+    y = gemm.linear_fwd(x, w)
+    assert y is not None
+    assert _rel(y, ref) < 1e-2
+    yb = gemm.linear_fwd(x, w, b)
+    assert _rel(yb, ref + b.float()) < 1e-2
+
+
+@pytest.mark.parametrize("erf", [False, True])
+@pytest.mark.parametrize("M,N,K", SHAPES[:3])
+def test_fwd_bias_gelu(gemm, M, N, K, erf):
+    torch.manual_seed(1)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    h_ref = x.float() @ w.float().t() + b.float()
+    y, h = gemm.linear_fwd(x, w, b, act="gelu_erf" if erf else "gelu")
+    assert _rel(h, h_ref) < 1e-2
+    assert _rel(y, _gelu(h_ref, erf)) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_dgrad(gemm, M, N, K, dtype):
+    # dx[M, K] = dy[M, N] @ w[N, K]
+    torch.manual_seed(2)
+    dy = torch.randn(M, N, device="cuda", dtype=dtype)
+    w = torch.randn(N, K, device="cuda", dtype=dtype) * 0.05
+    if N % 64 or K % 8:
+        assert gemm.linear_dgrad(dy, w) is None
+        return
+    dx = gemm.linear_dgrad(dy, w)
+    assert dx is not None
+    assert _rel(dx, dy.float() @ w.float()) < 1e-2
+
+
+@pytest.mark.parametrize("erf", [False, True])
+def test_dgrad_dgelu(gemm, erf):
+    torch.manual_seed(3)
+    M, N, K = 512, 1024, 768
+    dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    h = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    dx = gemm.linear_dgrad(dy, w, act_input=h, act="gelu_erf" if erf else "gelu")
+    ref = (dy.float() @ w.float()) * _gelu_grad(h.float(), erf)
+    assert _rel(dx, ref) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1024, 768, 512), (320, 520, 296),
+                                   (2048, 1000, 256)])
+def test_wgrad_f32(gemm, M, N, K, dtype):
+    # out[N, K] (+)= dy[M, N]^T x[M, K]  -- reduction over the M tokens
+    torch.manual_seed(4)
+    dy = torch.randn(M, N, device="cuda", dtype=dtype)
+    x = torch.randn(M, K, device="cuda", dtype=dtype)
+    out = torch.randn(N, K, device="cuda", dtype=torch.float32)
+    base = out.clone()
+    ref = dy.float().t() @ x.float()
+    if M % 64:
+        assert not gemm.linear_wgrad(dy, x, out, False)
+        return
+    assert gemm.linear_wgrad(dy, x, out, False)
+    assert _rel(out, ref) < 1e-4
+    out.copy_(base)
+    assert gemm.linear_wgrad(dy, x, out, True)
+    assert _rel(out, ref + base) < 1e-4
+
+
+def test_strided_rows(gemm):
+    """Row-strided activations (a column slice of a wider buffer) are read in place."""
+    torch.manual_seed(5)
+    big = torch.randn(512, 1024, device="cuda", dtype=torch.bfloat16)
+    x = big[:, 256:768]
+    w = torch.randn(384, 512, device="cuda", dtype=torch.bfloat16) * 0.05
+    y = gemm.linear_fwd(x, w)
+    assert _rel(y, x.float() @ w.float().t()) < 1e-2
+
+
+def test_uncovered_shapes_fall_back(gemm):
+    x = torch.randn(64, 100, device="cuda", dtype=torch.bfloat16)   # K % 64 != 0
+    w = torch.randn(128, 100, device="cuda", dtype=torch.bfloat16)
+    assert gemm.linear_fwd(x, w) is None
+    xf = torch.randn(64, 128, device="cuda")
+    assert gemm.linear_fwd(xf, xf) is None
+
+
+def test_gelu_without_bias(gemm):
+    torch.manual_seed(6)
+    x = torch.randn(512, 256, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(768, 256, device="cuda", dtype=torch.bfloat16) * 0.05
+    h_ref = x.float() @ w.float().t()
+    y, h = gemm.linear_fwd(x, w, None, act="gelu")
+    assert _rel(h, h_ref) < 1e-2
+    assert _rel(y, _gelu(h_ref, False)) < 1e-2
+
+
+@pytest.mark.parametrize("K", [128, 192])
+def test_persistent_many_tiles(gemm, K):
+    """More tiles than CUs: each workgroup walks several tiles with the staging
+    stream running across tile boundaries (odd and even K-tile counts)."""
+    torch.manual_seed(7)
+    M, N = 4608, 4352                     # 18 x 17 = 306 tiles of 256x256
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    ref = x.float() @ w.float().t() + b.float()
+    assert _rel(gemm.linear_fwd(x, w, b), ref) < 1e-2
+    y, h = gemm.linear_fwd(x, w, b, act="gelu")
+    assert _rel(h, ref) < 1e-2 and _rel(y, _gelu(ref, False)) < 1e-2
+    # dgrad over the same sizes: dx[M, K2] = dy[M, N] w2[N, K2] with N % 64 == 0
+    w2 = torch.randn(N, 4352, device="cuda", dtype=torch.bfloat16) * 0.05
+    dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    hh = torch.randn(M, 4352, device="cuda", dtype=torch.bfloat16)
+    dx = gemm.linear_dgrad(dy, w2, act_input=hh)
+    assert _rel(dx, (dy.float() @ w2.float()) * _gelu_grad(hh.float(), False)) < 1e-2
+    # wgrad with accumulate: out[N, K] += dy^T x over M tokens
+    out = torch.randn(N, K, device="cuda", dtype=torch.float32)
+    base = out.clone()
+    assert gemm.linear_wgrad(dy, x, out, True)
+    assert _rel(out, dy.float().t() @ x.float() + base) < 1e-4

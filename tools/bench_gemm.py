@@ -33,8 +33,10 @@ def main():
     ap.add_argument("--hidden", type=int, default=4096)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="", help="comma list of case names")
+    ap.add_argument("--variants", default="", help="comma list of HIP GEMM K-loop variants to A/B")
     a = ap.parse_args()
     from fleetx_amd.ops.elementwise import transpose2d
+    from fleetx_amd.ops import gemm as G
     M, h = a.tokens, a.hidden
     dev, bf = "cuda", torch.bfloat16
     shapes = {"qkv": (h, 3 * h), "out": (h, h), "fc1": (h, 4 * h), "fc2": (4 * h, h)}
@@ -44,6 +46,8 @@ def main():
         wt = w.t().contiguous()                                   # [in, out]
         dy = torch.randn(M, N, device=dev, dtype=bf)
         dw32 = torch.empty(N, K, device=dev, dtype=torch.float32)
+        bias = torch.randn(N, device=dev, dtype=bf) * 0.1
+        hpre = torch.randn(M, K, device=dev, dtype=bf)
         dyT = dy.t().contiguous()                                 # [N, M]
         xT = x.t().contiguous()                                   # [K, M]
         fl = 2.0 * M * N * K
@@ -67,10 +71,28 @@ def main():
             "transpose_dy_hip": lambda: transpose2d(dy, out=dyT),
             "wgrad_tn_path": lambda: torch.ops.aten.addmm.dtype_out(
                 dw32, transpose2d(dy), transpose2d(x).t(), torch.float32, out=dw32),
+            "dgrad_tn_path": lambda: torch.nn.functional.linear(dy, transpose2d(w)),
+            # hand-written MFMA GEMM (csrc/kernels/gemm.hip), native layouts
+            "hip_fwd": lambda: G.linear_fwd(x, w),
+            "hip_fwd_bias": lambda: G.linear_fwd(x, w, bias),
+            "hip_fwd_gelu": lambda: G.linear_fwd(x, w, bias, act="gelu"),
+            "hip_dgrad": lambda: G.linear_dgrad(dy, w),
+            "hip_dgrad_dgelu": lambda: G.linear_dgrad(dy, w, act_input=hpre),
+            "hip_wgrad_f32acc": lambda: G.linear_wgrad(dy, x, dw32, True),
         }
+        variants = [int(v) for v in a.variants.split(",")] if a.variants else [None]
+        items = []
         for k, fn in cases.items():
             if a.only and k not in a.only.split(","):
                 continue
+            if k.startswith("hip_"):
+                items += [(k if v is None else "%s_v%d" % (k, v), fn, v) for v in variants]
+            else:
+                items.append((k, fn, None))
+        for k, fn, v in items:
+            if v is not None:
+                from fleetx_amd.ops import _lib
+                _lib.kernels().gemm_set_variant(v)
             ms = timeit(fn, a.iters)
             # TFLOP/s of the GEMM (for transposes: us per call)
             res[k] = round(ms * 1e3, 1) if k.startswith("transpose") else round(fl / ms / 1e9, 1)
