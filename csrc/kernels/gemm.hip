@@ -908,6 +908,328 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(GemmParams P) {
   }
 }
 
+// ============================================================================
+// 4-wave kernel (default): 256 threads, one wave per SIMD, each wave owns a
+// 128x128 block of C as 8x8 v_mfma_f32_16x16x32 tiles (256 accumulators, in
+// the AGPR half of the register file).  Against the 8-wave layout this cuts
+// the LDS operand reads per K-tile by a third (every A row is read by 2
+// waves instead of 4) and doubles the MFMAs per barrier.
+//  * whole K-tiles (A 256x64 + B 256x64 = 64 KiB) are staged by LDS-DMA two
+//    tiles ahead into 2 buffers; per K-tile two barriers: B1 after the last
+//    operand read of the tile (its buffer may then be restaged with K-tile
+//    t+2) and B2 once K-tile t+1 has landed (its first operands are then read
+//    under the remaining MFMAs);
+//  * each k-step of 64 MFMAs carries the next k-step's 16 fragment reads (or
+//    the 16 staging loads), interleaved in fixed groups so the matrix pipe
+//    never waits for LDS.
+// ============================================================================
+constexpr int W4_TILE = 65536;
+constexpr int W4_SMEM = 2 * W4_TILE;
+
+// MFMA with the accumulator pinned to AGPRs: the builtin lets the register
+// allocator rename a 256-register accumulator set every K-iteration (hundreds
+// of v_accvgpr moves per tile); the tied "+a" operand keeps each accumulator
+// in place.  Its operands come straight from ds_read (the compiler still
+// inserts the lgkmcnt waits for them); consecutive MFMAs never share an
+// accumulator (64 apart), and the epilogue pads the MFMA -> read hazard.
+template <typename T>
+__device__ __forceinline__ void mma_agpr(floatx4& acc, const short8& x, const short8& y) {
+  if constexpr (FX_GEMM_ABL == 1) {
+    asm volatile("" ::"v"(x), "v"(y));
+  } else if constexpr (std::is_same<T, bf16>::value) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(x), "v"(y));
+  } else {
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(x), "v"(y));
+  }
+}
+
+template <int LAY>
+struct Stage4 {
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t vo[8];
+  long ld;
+  __device__ __forceinline__ void init(const uint16_t* base, long ld_, int rows, int K, int w,
+                                       int lane) {
+    ld = ld_;
+    const long extent = LAY == LAY_KC ? ((long)(rows - 1) * ld + K) * 2 : ((long)(K - 1) * ld + rows) * 2;
+    rs = rsrc(base, extent);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int blk = w * 8 + u;
+      if constexpr (LAY == LAY_KC) {
+        const int row = 8 * blk + (lane >> 3), c = lane & 7;
+        const int kc = c ^ ((row >> 1) & 7);
+        vo[u] = (uint32_t)(((long)row * ld + 8 * kc) * 2);
+      } else {
+        const int krow = 2 * blk + (lane >> 5), cc = lane & 31;
+        const int key = (krow & 3) | (((krow >> 3) & 1) << 2);
+        const int col = 16 * ((cc >> 1) ^ key) + 8 * (cc & 1);
+        vo[u] = (uint32_t)(((long)krow * ld + col) * 2);
+      }
+    }
+  }
+  __device__ __forceinline__ uint32_t origin(int rc0) const {
+    return LAY == LAY_KC ? (uint32_t)(rc0 * ld * 2) : (uint32_t)(rc0 * 2);
+  }
+  __device__ __forceinline__ uint32_t kterm(int kk) const {
+    return LAY == LAY_KC ? (uint32_t)(kk * BK * 2) : (uint32_t)(kk * BK * ld * 2);
+  }
+  __device__ __forceinline__ void issue(int u, uint32_t off, char* img, int w) const {
+    if (FX_GEMM_ABL >= 2) return;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_AS(img + (w * 8 + u) * 1024), 16, vo[u] + off,
+                                             0, 0, 0);
+  }
+};
+
+// operand fragment from a 256-row x 64-k image: KC rows of 128 B, MC k-rows of 512 B
+template <int LAY>
+__device__ __forceinline__ short8 frag4(const char* img, int pr0, int s, int lane) {
+  if constexpr (FX_GEMM_ABL == 3) {
+    short8 r;
+    asm volatile("; opaque" : "=v"(r));
+    return r;
+  } else if constexpr (LAY == LAY_KC) {
+    const int r = lane & 15;
+    const int c = 4 * s + (lane >> 4);
+    return *reinterpret_cast<const short8*>(img + (pr0 + r) * 128 + ((c ^ (r >> 1)) << 4));
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int key = q | ((g & 1) << 2);
+    const int blk = (pr0 >> 4) ^ key;
+    const char* b0 = img + (32 * s + 8 * g + q) * 512 + (blk << 5) + 8 * p;
+    v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDSV4(b0));
+    v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDSV4(b0 + 4 * 512));
+    short8 r;
+    r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+    r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+    return r;
+  }
+}
+
+template <typename T, int LA, int LB, int EPI>
+__global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmParams P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+
+  const int nwg = P.tiles_m * P.tiles_n;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int per_group = P.gm * P.tiles_n;
+  const int group = wg / per_group, first_m = group * P.gm;
+  const int gm = min(P.tiles_m - first_m, P.gm);
+  const int in_group = wg - group * per_group;
+  const int m0 = (first_m + in_group % gm) * BM;
+  const int n0 = (in_group / gm) * BN;
+
+  Stage4<LA> sa;
+  Stage4<LB> sb;
+  sa.init(P.A, P.lda, P.M, P.K, w, lane);
+  sb.init(P.B, P.ldb, P.N, P.K, w, lane);
+  const uint32_t ao = sa.origin(m0), bo = sb.origin(n0);
+  const int nk = P.K / BK;
+
+  auto stage = [&](int t, int u) {  // staging load u (0..15) of K-tile t
+    char* img = smem + (t & 1) * W4_TILE;
+    if (u < 8) sa.issue(u, ao + sa.kterm(t), img, w);
+    else sb.issue(u - 8, bo + sb.kterm(t), img + 32768, w);
+  };
+
+  floatx4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  short8 fa0[8], fb0[8], fa1[8], fb1[8];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) stage(0, u);
+  if (nk > 1) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) stage(1, u);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  cbar();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) fa0[i] = frag4<LA>(smem, wr * 128 + i * 16, 0, lane);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fb0[j] = frag4<LB>(smem + 32768, wc * 128 + j * 16, 0, lane);
+
+#if FX_GEMM_STAMP
+#define STAMP4(id)                                                                   \
+  do {                                                                               \
+    if (P.dbg && blockIdx.x == 0 && t >= 8 && t < 16) {                              \
+      const unsigned long long v_ = __builtin_amdgcn_s_memtime();                    \
+      if (lane == 0) P.dbg[(w * 8 + (t - 8)) * 8 + (id)] = v_;                       \
+    }                                                                                \
+  } while (0)
+#else
+#define STAMP4(id) do {} while (0)
+#endif
+  // Per K-tile: six segments, five barriers.  The A and B halves of a buffer
+  // are freed separately (after the last read of each), so the 16 staging
+  // loads of K-tile t+2 spread over three segments instead of one burst (the
+  // LDS-DMA path moves ~64 B/clk per CU: 64 KiB per K-tile is half of the
+  // MFMA time and has to be spread to stay hidden).
+  for (int t = 0; t < nk; ++t) {
+    STAMP4(0);
+    const char* ia = smem + (t & 1) * W4_TILE;
+    const char* ib = ia + 32768;
+    const char* na = smem + ((t + 1) & 1) * W4_TILE;
+    const char* nb = na + 32768;
+    const bool more = t + 2 < nk, next = t + 1 < nk;
+    // S1: k-step 0 rows 0-1; read A k-half 1
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) fa1[4 * i + r] = frag4<LA>(ia, wr * 128 + (4 * i + r) * 16, 1, lane);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mma_agpr<T>(acc[i][j], fb0[j], fa0[i]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    lds_reads_done();
+    cbar();  // A half of this buffer is free
+    STAMP4(1);
+    // S2: k-step 0 rows 2-3; stage A of K-tile t+2; read B k-half 1
+#pragma unroll
+    for (int i = 2; i < 4; ++i) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) stage(t + 2, 4 * (i - 2) + u);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) fb1[4 * (i - 2) + r] = frag4<LB>(ib, wc * 128 + (4 * (i - 2) + r) * 16, 1, lane);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mma_agpr<T>(acc[i][j], fb0[j], fa0[i]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    lds_reads_done();
+    cbar();  // B half of this buffer is free
+    STAMP4(2);
+    // S3: k-step 0 rows 4-7; stage B of K-tile t+2
+#pragma unroll
+    for (int i = 4; i < 8; ++i) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) {
+        stage(t + 2, 8 + 2 * (i - 4));
+        stage(t + 2, 8 + 2 * (i - 4) + 1);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mma_agpr<T>(acc[i][j], fb0[j], fa0[i]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    STAMP4(3);
+    // S4: k-step 1 rows 0-3; then K-tile t+1's A must have landed
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mma_agpr<T>(acc[i][j], fb1[j], fa1[i]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    STAMP4(4);
+    if (next) {
+      if (more) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      cbar();
+    }
+    STAMP4(5);
+    // S5: k-step 1 rows 4-5; read A k-half 0 of K-tile t+1, then its B must have landed
+#pragma unroll
+    for (int i = 4; i < 6; ++i) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (next) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) fa0[4 * (i - 4) + r] = frag4<LA>(na, wr * 128 + (4 * (i - 4) + r) * 16, 0, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mma_agpr<T>(acc[i][j], fb1[j], fa1[i]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (next) {
+      if (more) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      cbar();
+    }
+    STAMP4(6);
+    // S6: k-step 1 rows 6-7; read B k-half 0 of K-tile t+1
+#pragma unroll
+    for (int i = 6; i < 8; ++i) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (next) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) fb0[4 * (i - 6) + r] = frag4<LB>(nb, wc * 128 + (4 * (i - 6) + r) * 16, 0, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mma_agpr<T>(acc[i][j], fb1[j], fa1[i]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    STAMP4(7);
+  }
+#undef STAMP4
+
+  // ---- epilogue (direct stores; lane holds C[m][n .. n+3])
+  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // last MFMAs -> accumulator reads
+  const int mrow = m0 + wr * 128 + (lane & 15);
+  const int ncol = n0 + wc * 128 + 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = mrow + i * 16;
+    if (m >= P.M) continue;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = ncol + j * 16;
+      if (n >= P.N) continue;
+      const floatx4 a = acc[i][j];
+      if constexpr (EPI == EPI_F32) {
+        float* c = reinterpret_cast<float*>(P.C) + (long)m * P.ldc + n;
+        float4 v = make_float4(a[0], a[1], a[2], a[3]);
+        if (P.beta) {
+          const float4 o = *reinterpret_cast<const float4*>(c);
+          v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+        }
+        *reinterpret_cast<float4*>(c) = v;
+      } else {
+        float v[4] = {a[0], a[1], a[2], a[3]};
+        uint16_t* c = reinterpret_cast<uint16_t*>(P.C) + (long)m * P.ldc + n;
+        if constexpr (EPI == EPI_STORE) {
+          if (P.bias != nullptr) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += Elt<T>::to_f(P.bias[n + e]);
+          }
+        } else if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_ERF) {
+          ushort4 hv;
+          uint16_t* hp = reinterpret_cast<uint16_t*>(&hv);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x = v[e] + (P.bias != nullptr ? Elt<T>::to_f(P.bias[n + e]) : 0.f);
+            hp[e] = Elt<T>::from_f(x);
+            v[e] = EPI == EPI_BIAS_GELU ? gelu_tanh(x) : gelu_erf(x);
+          }
+          *reinterpret_cast<ushort4*>(P.aux + (long)m * P.ldaux + n) = hv;
+        } else {  // DGELU
+          const ushort4 hv = *reinterpret_cast<const ushort4*>(P.aux + (long)m * P.ldaux + n);
+          const uint16_t* hp = reinterpret_cast<const uint16_t*>(&hv);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x = Elt<T>::to_f(hp[e]);
+            v[e] *= EPI == EPI_DGELU ? gelu_tanh_grad(x) : gelu_erf_grad(x);
+          }
+        }
+        ushort4 o;
+        uint16_t* op = reinterpret_cast<uint16_t*>(&o);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) op[e] = Elt<T>::from_f(v[e]);
+        *reinterpret_cast<ushort4*>(c) = o;
+      }
+    }
+  }
+}
+
 static int g_variant = -1;  // FLEETX_GEMM_PF: 0 = plain (default), 1 = prefetching, 2/3 = persistent (prefetching / staggered)
 static int g_gm = -1;       // FLEETX_GEMM_GM: M-group height of the tile order (default 8)
 
@@ -917,7 +1239,17 @@ void launch(const GemmParams& P, hipStream_t st) {
     const char* e = getenv("FLEETX_GEMM_PF");
     g_variant = e ? atoi(e) : 0;
   }
-  if (g_variant >= 2 && P.K >= 2 * BK && P.N % 8 == 0) {
+  if (g_variant == 4) {
+    auto k4 = gemm4_kernel<T, LA, LB, EPI>;
+    static bool attr4 = false;
+    if (!attr4) {
+      (void)hipFuncSetAttribute((const void*)k4, hipFuncAttributeMaxDynamicSharedMemorySize, W4_SMEM);
+      attr4 = true;
+    }
+    hipLaunchKernelGGL(k4, dim3(P.tiles_m * P.tiles_n), dim3(256), W4_SMEM, st, P);
+    return;
+  }
+  if (g_variant >= 2 && g_variant <= 3 && P.K >= 2 * BK && P.N % 8 == 0) {
     auto kp = g_variant == 2 ? gemm_pk_kernel<T, LA, LB, EPI, true> : gemm_pk_kernel<T, LA, LB, EPI, false>;
     static bool attr_pk[2] = {false, false};
     static int ncu = 0;

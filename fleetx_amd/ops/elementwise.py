@@ -86,8 +86,10 @@ def gelu_plain(h, erf=False):
     return _gelu_ref(h.float(), erf).to(h.dtype)
 
 
-def gelu_grad(dy, h, erf=False):
-    """``dy * gelu'(h)`` without autograd (fallback of the fused dGeLU epilogue)."""
+def gelu_grad(dy, h, erf=False, colsum=None):
+    """``dy * gelu'(h)`` without autograd (fallback of the fused dGeLU epilogue).
+    ``colsum = (dst_f32, accumulate)`` also writes / adds the column sums of the
+    result (a bias gradient) from the same pass."""
     dy = dy.contiguous()
     h = h.contiguous()
     if dy.is_cuda:
@@ -97,10 +99,20 @@ def gelu_grad(dy, h, erf=False):
         splits = k.coltile_splits(rows, cols)
         part = torch.empty(splits, cols, device=h.device, dtype=torch.float32)
         dx = torch.empty_like(h)
-        k.bias_gelu_bwd(_lib.dt_code(h.dtype), int(erf), dy.data_ptr(), h.data_ptr(), 0,
+        dc = _lib.dt_code(h.dtype)
+        k.bias_gelu_bwd(dc, int(erf), dy.data_ptr(), h.data_ptr(), 0,
                         dx.data_ptr(), part.data_ptr(), rows, cols, splits, _lib.stream())
+        if colsum is not None:
+            dst, acc = colsum
+            k.coltile_finalize(dc, part.data_ptr(), splits, cols, dst.data_ptr(), 0, int(acc),
+                               _lib.stream())
         return dx
-    return (dy.float() * _gelu_grad_ref(h.float(), erf)).to(h.dtype)
+    dx = (dy.float() * _gelu_grad_ref(h.float(), erf)).to(h.dtype)
+    if colsum is not None:
+        dst, acc = colsum
+        s = dx.float().reshape(-1, dst.numel()).sum(0).view_as(dst)
+        dst.add_(s) if acc else dst.copy_(s)
+    return dx
 
 
 class _BiasDropoutAdd(torch.autograd.Function):

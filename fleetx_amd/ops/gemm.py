@@ -46,11 +46,14 @@ def set_mode(mode):
 
 # GEMM kinds routed to the MFMA kernel under FLEETX_GEMM=auto (kinds where it
 # beats hipBLASLt incl. the transposes hipBLASLt needs; tools/bench_gemm.py)
-AUTO_KINDS = set(k for k in os.environ.get("FLEETX_GEMM_AUTO", "wgrad").split(",") if k)
+# Measured on the 6.7B step (profiles/r2_gemm/): every kind currently costs
+# 8-17 ms/step against hipBLASLt, so none is routed by default.
+AUTO_KINDS = set(k for k in os.environ.get("FLEETX_GEMM_AUTO", "").split(",") if k)
 
 
 def use(kind, a, b=None):
-    """Whether GEMM ``kind`` ('fwd' | 'dgrad' | 'wgrad') on these operands goes
+    """Whether GEMM ``kind`` ('fwd' | 'fwd_act' | 'dgrad' | 'dgrad_act' |
+    'wgrad'; ``_act`` = with the GeLU / GeLU' epilogue) on these operands goes
     to the MFMA kernel (the kernel itself may still decline the shape)."""
     if _MODE == "blas" or not a.is_cuda or a.dtype not in (torch.bfloat16, torch.float16):
         return False

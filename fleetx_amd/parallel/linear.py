@@ -168,18 +168,25 @@ def fwd_gemm(x, weight, bias=None):
     return F.linear(x, weight, bias)
 
 
-def dgrad_gemm(dy, w, act_input=None, act="gelu"):
-    """``dy @ w`` (times ``gelu'(act_input)`` when given) on the MFMA kernel."""
-    if G.use("dgrad", dy, w):
+def dgrad_gemm(dy, w, act_input=None, act="gelu", colsum=None):
+    """``dy @ w`` (times ``gelu'(act_input)`` when given) on the MFMA kernel.
+    ``colsum = (dst_f32, accumulate)``: column sums of the result as well (the
+    fallback takes them from the dGeLU pass; the caller reduces otherwise and
+    gets ``done = False`` back through ``colsum_done``)."""
+    if G.use("dgrad" if act_input is None else "dgrad_act", dy, w):
         dy2 = dy.reshape(-1, dy.shape[-1])
         ai = None if act_input is None else act_input.reshape(-1, act_input.shape[-1])
         dx = G.linear_dgrad(dy2, w, act_input=ai, act=act)
         if dx is not None:
+            if colsum is not None:
+                colsum_into(dx, colsum[0], colsum[1])
             return dx.view(*dy.shape[:-1], w.shape[1])
     dx = dgrad(dy, w)
     if act_input is not None:
         from ..ops.elementwise import gelu_grad
-        dx = gelu_grad(dx, act_input, erf=(act != "gelu"))
+        dx = gelu_grad(dx, act_input, erf=(act != "gelu"), colsum=colsum)
+    elif colsum is not None:
+        colsum_into(dx.reshape(-1, dx.shape[-1]), colsum[0], colsum[1])
     return dx
 
 
@@ -319,7 +326,7 @@ class _FusedMLP(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, act):
         ctx.act = act
         x2 = x.reshape(-1, x.shape[-1])
-        r = G.linear_fwd(x2, w1, b1, act=act) if G.use("fwd", x2, w1) else None
+        r = G.linear_fwd(x2, w1, b1, act=act) if G.use("fwd_act", x2, w1) else None
         if r is None:
             from ..ops.elementwise import gelu_plain
             h = F.linear(x2, w1, b1)
@@ -338,18 +345,22 @@ class _FusedMLP(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         x2 = x.reshape(-1, x.shape[-1])
         dw2 = _wgrad(w2, dy2, a)
-        dh = dgrad_gemm(dy2, w2, act_input=h, act=ctx.act)
-        db1 = None
+        # db1 = colsum(dH) from the same pass as dH where possible; fp32 straight
+        # into main_grad when the bias lives in the flat buffer
+        db1, cs, into_main = None, None, False
         if b1 is not None:
-            # the bias takes its fp32 grad directly when it lives in the buffer
             if hasattr(b1, "main_grad") and getattr(b1, "_fx_grad_ready", None) is not None:
-                colsum_into(dh, b1.main_grad, not getattr(b1, "_fx_fresh", False))
+                cs = (b1.main_grad, not getattr(b1, "_fx_fresh", False))
+                into_main = True
+            else:
+                cs = (torch.empty(b1.shape, device=dy.device, dtype=torch.float32), False)
+        dh = dgrad_gemm(dy2, w2, act_input=h, act=ctx.act, colsum=cs)
+        if b1 is not None:
+            if into_main:
                 b1._fx_fresh = False
                 grad_part_done(b1)
             else:
-                t = torch.empty(b1.shape, device=dh.device, dtype=torch.float32)
-                colsum_into(dh, t, False)
-                db1 = t.to(b1.dtype)
+                db1 = cs[0].to(b1.dtype)
         dw1 = _wgrad(w1, dh, x2)
         dx = dgrad_gemm(dh, w1)
         return dx.view_as(x), dw1, db1, dw2, None

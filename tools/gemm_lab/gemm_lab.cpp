@@ -72,7 +72,7 @@ int main(int argc, char** argv) {
         char want[64];
         snprintf(want, sizeof(want), "%s:%s", s.name, c.nm);
         if (!strcmp(want, stamp_case)) {
-          const int nst = 8 * 8 * 4 * 6;
+          const int nst = 8 * 8 * 4 * 6;  // also covers 4 waves x 8 K-tiles x 8 stamps
           unsigned long long* d;
           CK(hipMalloc(&d, nst * 8));
           CK(hipMemset(d, 0, nst * 8));
