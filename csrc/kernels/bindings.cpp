@@ -34,17 +34,17 @@ void fx_ce_bwd(int, const void*, void*, const int64_t*, const float*, const floa
 int fx_sumsq_blocks(long n);
 void fx_sumsq_f32(const float*, long, float*, int, hipStream_t);
 void fx_adamw_flat(int, float*, const float*, float*, float*, void*, long, float, float, float,
-                   float, float, float, float, const float*, const int*, hipStream_t);
+                   float, float, float, const float*, const int*, const int*, hipStream_t);
 void fx_cast_f32(int, const float*, void*, long, hipStream_t);
 void fx_accum_f32(int, float*, const void*, long, int, hipStream_t);
 void fx_embedding_fwd(int, const int64_t*, const int64_t*, const void*, const void*, void*, int,
                       int, long, long, hipStream_t);
 void fx_embedding_bwd(int, const int64_t*, const void*, float*, int, int, long, long,
                       hipStream_t);
-int fx_flash_fwd(const void*, const void*, const void*, void*, float*, const long*, const long*,
+int fx_flash_fwd(int, const void*, const void*, const void*, void*, float*, const long*, const long*,
                  const long*, const long*, const int*, const float*, long, int, int, int, int, int,
                  int, float, float, uint64_t, hipStream_t);
-int fx_flash_bwd(const void*, const void*, const void*, const void*, const void*, const float*,
+int fx_flash_bwd(int, const void*, const void*, const void*, const void*, const void*, const float*,
                  float*, void*, void*, void*, const long*, const long*, const long*, const long*,
                  const long*, const long*, const int*, const float*, long, int, int, int, int, int,
                  int, float, float, uint64_t, hipStream_t);
@@ -62,8 +62,8 @@ int fx_gn_bwd_apply(int, const void*, const void*, const float*, const float*, c
 int fx_transpose16(int, const void*, void*, float*, int, int, long, long, hipStream_t);
 int fx_sample(int, const void*, long, int, int, float, int, float, const float*, int64_t*, float*,
               float*, hipStream_t);
-int fx_decode_attn(const void*, const void*, const void*, void*, const int*, int, int, int, int,
-                   int, long, long, long, long, long, long, float, hipStream_t);
+int fx_decode_attn(int, const void*, const void*, const void*, void*, const int*, int, int, int,
+                   int, int, float*, long, long, long, long, long, long, float, hipStream_t);
 void fx_embedding_bwd_sorted(int, const int64_t*, const int64_t*, const void*, float*, int, int,
                              long, long, hipStream_t);
 int fx_softmax_fwd(int, int, const void*, const void*, void*, long, int, int, long, float, int,
@@ -141,10 +141,10 @@ PYBIND11_MODULE(_kernels, m) {
     fx_sumsq_f32(F(x), n, F(partial), blocks, S(st));
   });
   m.def("adamw_flat", [](int dt, ptr p, ptr g, ptr mm, ptr vv, ptr p16, long n, float lr,
-                         float b1, float b2, float eps, float wd, float bc1, float bc2, ptr gscale,
-                         ptr skip, ptr st) {
-    fx_adamw_flat(dt, F(p), F(g), F(mm), F(vv), P(p16), n, lr, b1, b2, eps, wd, bc1, bc2,
-                  F(gscale), reinterpret_cast<const int*>(skip), S(st));
+                         float b1, float b2, float eps, float wd, float l2, ptr gscale, ptr skip,
+                         ptr step, ptr st) {
+    fx_adamw_flat(dt, F(p), F(g), F(mm), F(vv), P(p16), n, lr, b1, b2, eps, wd, l2, F(gscale),
+                  reinterpret_cast<const int*>(skip), reinterpret_cast<const int*>(step), S(st));
   });
   m.def("cast_f32", [](int dt, ptr x, ptr y, long n, ptr st) {
     fx_cast_f32(dt, F(x), P(y), n, S(st));
@@ -169,22 +169,23 @@ PYBIND11_MODULE(_kernels, m) {
                             reinterpret_cast<const int64_t*>(perm), CP(dout), F(dW), ntok, h,
                             vstart, vsize, S(st));
   });
-  m.def("flash_fwd", [](ptr q, ptr k, ptr v, ptr out, ptr lse, std::vector<long> qs,
+  m.def("flash_fwd", [](int dt, ptr q, ptr k, ptr v, ptr out, ptr lse, std::vector<long> qs,
                         std::vector<long> ks, std::vector<long> vs, std::vector<long> os,
                         ptr kv_lens, ptr kbias, long kb_stride, int B, int H, int Sq, int Sk, int D,
                         int causal, float scale, float p, uint64_t key, ptr st) {
     auto a = v3(qs), b = v3(ks), c = v3(vs), d = v3(os);
-    return fx_flash_fwd(CP(q), CP(k), CP(v), P(out), F(lse), a.data(), b.data(), c.data(),
+    return fx_flash_fwd(dt, CP(q), CP(k), CP(v), P(out), F(lse), a.data(), b.data(), c.data(),
                         d.data(), reinterpret_cast<const int*>(kv_lens), F(kbias), kb_stride, B, H,
                         Sq, Sk, D, causal, scale, p, key, S(st));
   });
-  m.def("flash_bwd", [](ptr q, ptr k, ptr v, ptr o, ptr dout, ptr lse, ptr delta, ptr dq, ptr dk,
+  m.def("flash_bwd", [](int dt, ptr q, ptr k, ptr v, ptr o, ptr dout, ptr lse, ptr delta, ptr dq,
+                        ptr dk,
                         ptr dv, std::vector<long> qs, std::vector<long> ks, std::vector<long> vs,
                         std::vector<long> os, std::vector<long> dqs, std::vector<long> dks,
                         ptr kv_lens, ptr kbias, long kb_stride, int B, int H, int Sq, int Sk, int D,
                         int causal, float scale, float p, uint64_t key, ptr st) {
     auto a = v3(qs), b = v3(ks), c = v3(vs), d = v3(os), e = v3(dks), f = v3(dqs);
-    return fx_flash_bwd(CP(q), CP(k), CP(v), CP(o), CP(dout), F(lse), F(delta), P(dq), P(dk),
+    return fx_flash_bwd(dt, CP(q), CP(k), CP(v), CP(o), CP(dout), F(lse), F(delta), P(dq), P(dk),
                         P(dv), a.data(), b.data(), c.data(), d.data(), f.data(), e.data(),
                         reinterpret_cast<const int*>(kv_lens), F(kbias), kb_stride, B, H, Sq, Sk,
                         D, causal, scale, p, key, S(st));
@@ -222,11 +223,11 @@ PYBIND11_MODULE(_kernels, m) {
     return fx_sample(dt, CP(logits), ld, B, V, inv_temp, top_k, top_p, F(u),
                      reinterpret_cast<int64_t*>(ids), F(lse), F(probs), S(st));
   });
-  m.def("decode_attn", [](ptr q, ptr kc, ptr vc, ptr out, ptr lens, int B, int H, int D,
-                          int maxlen, int nsplit, long sqb, long sqh, long skb, long sks, long skh,
-                          long sob, float scale, ptr st) {
-    return fx_decode_attn(CP(q), CP(kc), CP(vc), P(out), reinterpret_cast<const int*>(lens), B, H,
-                          D, maxlen, nsplit, sqb, sqh, skb, sks, skh, sob, scale, S(st));
+  m.def("decode_attn", [](int dt, ptr q, ptr kc, ptr vc, ptr out, ptr lens, int B, int H, int D,
+                          int maxlen, int nsplit, ptr ws, long sqb, long sqh, long skb, long sks,
+                          long skh, long sob, float scale, ptr st) {
+    return fx_decode_attn(dt, CP(q), CP(kc), CP(vc), P(out), reinterpret_cast<const int*>(lens), B,
+                          H, D, maxlen, nsplit, F(ws), sqb, sqh, skb, sks, skh, sob, scale, S(st));
   });
   m.def("softmax_fwd", [](int dt, int mdt, ptr x, ptr mask, ptr y, long rows, int Sq, int Sk,
                           long mask_div, float scale, int causal, ptr st) {

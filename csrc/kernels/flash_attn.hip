@@ -22,6 +22,8 @@
 //    tile i computes, one vmcnt drain + barrier per tile.
 //  * blockIdx is remapped so the q-blocks of one (batch, head) run on one XCD
 //    (shared K/V stay in that XCD's L2); causal heavy blocks go first.
+#include <type_traits>
+
 #include "fx_common.h"
 
 typedef short v4s __attribute__((ext_vector_type(4)));
@@ -46,14 +48,14 @@ __device__ __forceinline__ int loff(int row, int ch) {
 
 // A/B fragment row read (32x32x16 operand): row r, k-step s, lane half h
 template <int D>
-__device__ __forceinline__ bf16x8 row_frag(const char* tile, int row, int s, int h) {
-  return *reinterpret_cast<const bf16x8*>(tile + loff<D>(row, 2 * s + h));
+__device__ __forceinline__ short8 row_frag(const char* tile, int row, int s, int h) {
+  return *reinterpret_cast<const short8*>(tile + loff<D>(row, 2 * s + h));
 }
 
 // Transposed fragment: lane gets column (dt*32 + (lane&31)) of rows
 // keybase+{0..3} and keybase+8+{0..3}; keybase includes 4*h.
 template <int D>
-__device__ __forceinline__ bf16x8 tr_frag(const char* tile, int keybase, int dt, int lane) {
+__device__ __forceinline__ short8 tr_frag(const char* tile, int keybase, int dt, int lane) {
   const int gi = (lane >> 4) & 1, i = lane & 15, q = i >> 2, p = i & 3;
   const int ch = dt * 4 + 2 * gi + (p >> 1);
   const int b0 = loff<D>(keybase + q, ch) + 8 * (p & 1);
@@ -63,11 +65,25 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int keybase, int dt,
   short8 r;
   r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-  return __builtin_bit_cast(bf16x8, r);
+  return r;
 }
 
-__device__ __forceinline__ floatx16 mfma(const bf16x8& a, const bf16x8& b, const floatx16& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+// bf16 or fp16 inputs (T), fp32 accumulate; the 16-bit operands travel as raw lanes
+template <typename T>
+__device__ __forceinline__ floatx16 mfma(const short8& a, const short8& b, const floatx16& c) {
+  if constexpr (std::is_same<T, bf16>::value)
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+// fp32 -> 16-bit lane of type T (round to nearest even)
+template <typename T>
+__device__ __forceinline__ short cvt16(float x) {
+  if constexpr (std::is_same<T, bf16>::value) return __builtin_bit_cast(short, (__bf16)x);
+  else return __builtin_bit_cast(short, (_Float16)x);
 }
 
 // row index (within a 32-row C tile) held in register i for lane half h
@@ -192,7 +208,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
 // ============================================================================
 // forward: WG = 4 waves x 32 queries = 128 queries; KV tile = 64 keys
 // ============================================================================
-template <int D, bool CAUSAL, bool DROP, bool KB>
+template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
 __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KV = 64, TB = KV * D * 2;
@@ -212,13 +228,13 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
 
   const int wq0 = qblock * 128 + w * 32;
   const int qi = wq0 + (lane & 31);
-  bf16x8 qf[D / 16];
+  short8 qf[D / 16];
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) {
     if (qi < P.Sq)
-      qf[s] = *reinterpret_cast<const bf16x8*>(qp + (long)qi * P.sq_s + 16 * s + 8 * h);
+      qf[s] = *reinterpret_cast<const short8*>(qp + (long)qi * P.sq_s + 16 * s + 8 * h);
     else
-      qf[s] = __builtin_bit_cast(bf16x8, (short8){0, 0, 0, 0, 0, 0, 0, 0});
+      qf[s] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
   }
 
   int kv_end = kv_len;
@@ -258,7 +274,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
       floatx16 sacc[2];
       // all K fragments of the tile up front: the 16 LDS reads overlap each
       // other instead of one exposed LDS latency per MFMA
-      bf16x8 kfr[2][D / 16];
+      short8 kfr[2][D / 16];
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -268,7 +284,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) sacc[t][i] = 0.f;
 #pragma unroll
-        for (int s = 0; s < D / 16; ++s) sacc[t] = mfma(kfr[t][s], qf[s], sacc[t]);
+        for (int s = 0; s < D / 16; ++s) sacc[t] = mfma<T>(kfr[t][s], qf[s], sacc[t]);
       }
       const bool need_mask = (CAUSAL && kb + KV - 1 > wq0) || (kb + KV > kv_len);
       float mloc = -INFINITY;
@@ -318,13 +334,13 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
-          bf16x8 pf;
+          short8 pf;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) pf[j] = (__bf16)sacc[t][8 * ss + j];
+          for (int j = 0; j < 8; ++j) pf[j] = cvt16<T>(sacc[t][8 * ss + j]);
           const int keybase = 32 * t + 16 * ss + 4 * h;
 #pragma unroll
           for (int dt = 0; dt < D / 32; ++dt)
-            oacc[dt] = mfma(tr_frag<D>(vt, keybase, dt, lane), pf, oacc[dt]);
+            oacc[dt] = mfma<T>(tr_frag<D>(vt, keybase, dt, lane), pf, oacc[dt]);
         }
     }
     glds_wait();
@@ -340,10 +356,10 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         ushort4 o;
-        o.x = float_to_bf16_bits(oacc[dt][4 * g + 0] * inv);
-        o.y = float_to_bf16_bits(oacc[dt][4 * g + 1] * inv);
-        o.z = float_to_bf16_bits(oacc[dt][4 * g + 2] * inv);
-        o.w = float_to_bf16_bits(oacc[dt][4 * g + 3] * inv);
+        o.x = Elt<T>::from_f(oacc[dt][4 * g + 0] * inv);
+        o.y = Elt<T>::from_f(oacc[dt][4 * g + 1] * inv);
+        o.z = Elt<T>::from_f(oacc[dt][4 * g + 2] * inv);
+        o.w = Elt<T>::from_f(oacc[dt][4 * g + 3] * inv);
         *reinterpret_cast<ushort4*>(op + dt * 32 + 8 * g + 4 * h) = o;
       }
     if (h == 0) P.lse[(long)bh * P.Sq + qi] = ltot > 0.f ? (m_run + log2f(ltot)) * LN2 : INFINITY;
@@ -353,7 +369,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
 // ============================================================================
 // backward preprocess: delta[bh, q] = sum_d dO * O
 // ============================================================================
-template <int D>
+template <typename T, int D>
 __global__ __launch_bounds__(256) void fa_bwd_pre_kernel(AttnParams P) {
   // 8 threads x 16B per row chunk of 64 elems; D/8 threads per row
   constexpr int TPR = D / 8;
@@ -367,8 +383,8 @@ __global__ __launch_bounds__(256) void fa_bwd_pre_kernel(AttnParams P) {
     const int b = bh / P.H, hd = bh % P.H;
     const long off = b * P.so_b + hd * P.so_h + (long)q * P.so_s + c;
     float a[8], g[8];
-    load8<bf16>(P.o + off, a);
-    load8<bf16>(P.dout + off, g);
+    load8<T>(P.o + off, a);
+    load8<T>(P.dout + off, g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += a[j] * g[j];
   }
@@ -381,7 +397,7 @@ __global__ __launch_bounds__(256) void fa_bwd_pre_kernel(AttnParams P) {
 // backward dQ: WG = 4 waves x 32 queries; loop over 64-key tiles.
 //   S^T = K.Q^T, dP^T = V.dO^T (queries on lanes), dQ^T += K^T.dS^T
 // ============================================================================
-template <int D, bool CAUSAL, bool DROP, bool KB>
+template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KV = 64, TB = KV * D * 2;
@@ -402,14 +418,14 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
   const int wq0 = qblock * 128 + w * 32;
   const int qi = wq0 + (lane & 31);
   const bool qvalid = qi < P.Sq;
-  bf16x8 qf[D / 16], gf[D / 16];
+  short8 qf[D / 16], gf[D / 16];
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) {
     if (qvalid) {
-      qf[s] = *reinterpret_cast<const bf16x8*>(qp + (long)qi * P.sq_s + 16 * s + 8 * h);
-      gf[s] = *reinterpret_cast<const bf16x8*>(dop + (long)qi * P.so_s + 16 * s + 8 * h);
+      qf[s] = *reinterpret_cast<const short8*>(qp + (long)qi * P.sq_s + 16 * s + 8 * h);
+      gf[s] = *reinterpret_cast<const short8*>(dop + (long)qi * P.so_s + 16 * s + 8 * h);
     } else {
-      qf[s] = __builtin_bit_cast(bf16x8, (short8){0, 0, 0, 0, 0, 0, 0, 0});
+      qf[s] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
       gf[s] = qf[s];
     }
   }
@@ -457,8 +473,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
         for (int i = 0; i < 16; ++i) sacc[i] = dpacc[i] = 0.f;
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
-          sacc = mfma(row_frag<D>(kt, 32 * t + (lane & 31), s, h), qf[s], sacc);
-          dpacc = mfma(row_frag<D>(vt, 32 * t + (lane & 31), s, h), gf[s], dpacc);
+          sacc = mfma<T>(row_frag<D>(kt, 32 * t + (lane & 31), s, h), qf[s], sacc);
+          dpacc = mfma<T>(row_frag<D>(vt, 32 * t + (lane & 31), s, h), gf[s], dpacc);
         }
         if constexpr (KB) key_bias_add1(sacc, P.kbias + (long)b * P.kb_b + kb + 32 * t, h, sl2);
 #pragma unroll
@@ -481,13 +497,13 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
         }
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
-          bf16x8 df;
+          short8 df;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) df[j] = (__bf16)sacc[8 * ss + j];
+          for (int j = 0; j < 8; ++j) df[j] = cvt16<T>(sacc[8 * ss + j]);
           const int keybase = 32 * t + 16 * ss + 4 * h;
 #pragma unroll
           for (int dt = 0; dt < D / 32; ++dt)
-            dqacc[dt] = mfma(tr_frag<D>(kt, keybase, dt, lane), df, dqacc[dt]);
+            dqacc[dt] = mfma<T>(tr_frag<D>(kt, keybase, dt, lane), df, dqacc[dt]);
         }
       }
     }
@@ -501,10 +517,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         ushort4 o;
-        o.x = float_to_bf16_bits(dqacc[dt][4 * g + 0] * P.scale);
-        o.y = float_to_bf16_bits(dqacc[dt][4 * g + 1] * P.scale);
-        o.z = float_to_bf16_bits(dqacc[dt][4 * g + 2] * P.scale);
-        o.w = float_to_bf16_bits(dqacc[dt][4 * g + 3] * P.scale);
+        o.x = Elt<T>::from_f(dqacc[dt][4 * g + 0] * P.scale);
+        o.y = Elt<T>::from_f(dqacc[dt][4 * g + 1] * P.scale);
+        o.z = Elt<T>::from_f(dqacc[dt][4 * g + 2] * P.scale);
+        o.w = Elt<T>::from_f(dqacc[dt][4 * g + 3] * P.scale);
         *reinterpret_cast<ushort4*>(dqp + dt * 32 + 8 * g + 4 * h) = o;
       }
   }
@@ -532,7 +548,7 @@ __device__ __forceinline__ uint32_t dpp_swap1(uint32_t v) {
 // hash per query row, so each lane hashes every other query row and the
 // pair trades results through DPP (one hash per two elements, as fwd / dQ).
 // ============================================================================
-template <int D, bool CAUSAL, bool DROP, bool KB>
+template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int QT = FA_DKDV_QT, TB = QT * D * 2;
@@ -557,13 +573,13 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
   const int ki = wk0 + (lane & 31);
   const bool kvalid = ki < kv_len;
   const float kb2 = KB ? P.kbias[(long)b * P.kb_b + ki] * LOG2E : 0.f;
-  bf16x8 kf[D / 16];
+  short8 kf[D / 16];
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) {
     if (ki < P.Sk)
-      kf[s] = *reinterpret_cast<const bf16x8*>(kp + (long)ki * P.sk_s + 16 * s + 8 * h);
+      kf[s] = *reinterpret_cast<const short8*>(kp + (long)ki * P.sk_s + 16 * s + 8 * h);
     else
-      kf[s] = __builtin_bit_cast(bf16x8, (short8){0, 0, 0, 0, 0, 0, 0, 0});
+      kf[s] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
   }
   // V rows of this WG's 128 keys -> LDS (rows past Sk clamp; those keys are masked)
   Glds<D, 128>::load(vp, P.sv_s, kblock * 128, P.Sk, vs, w, lane);
@@ -648,15 +664,15 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
         for (int i = 0; i < 16; ++i) sacc[i] = dpacc[i] = 0.f;
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
-          sacc = mfma(row_frag<D>(qt, 32 * t + (lane & 31), s, h), kf[s], sacc);
-          dpacc = mfma(row_frag<D>(gt, 32 * t + (lane & 31), s, h),
+          sacc = mfma<T>(row_frag<D>(qt, 32 * t + (lane & 31), s, h), kf[s], sacc);
+          dpacc = mfma<T>(row_frag<D>(gt, 32 * t + (lane & 31), s, h),
                        row_frag<D>(vs, 32 * w + (lane & 31), s, h), dpacc);
         }
         // P o Z (for dV) and dS (for dK) straight to bf16, one 8-row half at a
         // time: no fp32 copies of the tile stay live across the MFMAs
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
-          bf16x8 pf, df;
+          short8 pf, df;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const int i = 8 * ss + j;
@@ -665,14 +681,14 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
             float p = fexp2(sacc[i] * sl2 + kb2 - lse_s[ql_]);
             if ((CAUSAL && ki > q) || !kvalid || q >= P.Sq) p = 0.f;
             const float z = DROP ? (((keep >> i) & 1u) ? P.drop_scale : 0.f) : 1.f;
-            pf[j] = (__bf16)(p * z);
-            df[j] = (__bf16)(p * (dpacc[i] * z - dl_s[ql_]));  // dS
+            pf[j] = cvt16<T>(p * z);
+            df[j] = cvt16<T>(p * (dpacc[i] * z - dl_s[ql_]));  // dS
           }
           const int qbase = 32 * t + 16 * ss + 4 * h;
 #pragma unroll
           for (int dt = 0; dt < D / 32; ++dt) {
-            dvacc[dt] = mfma(tr_frag<D>(gt, qbase, dt, lane), pf, dvacc[dt]);
-            dkacc[dt] = mfma(tr_frag<D>(qt, qbase, dt, lane), df, dkacc[dt]);
+            dvacc[dt] = mfma<T>(tr_frag<D>(gt, qbase, dt, lane), pf, dvacc[dt]);
+            dkacc[dt] = mfma<T>(tr_frag<D>(qt, qbase, dt, lane), df, dkacc[dt]);
           }
         }
       }
@@ -689,14 +705,14 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         ushort4 a, c;
-        a.x = float_to_bf16_bits(dkacc[dt][4 * g + 0] * P.scale);
-        a.y = float_to_bf16_bits(dkacc[dt][4 * g + 1] * P.scale);
-        a.z = float_to_bf16_bits(dkacc[dt][4 * g + 2] * P.scale);
-        a.w = float_to_bf16_bits(dkacc[dt][4 * g + 3] * P.scale);
-        c.x = float_to_bf16_bits(dvacc[dt][4 * g + 0]);
-        c.y = float_to_bf16_bits(dvacc[dt][4 * g + 1]);
-        c.z = float_to_bf16_bits(dvacc[dt][4 * g + 2]);
-        c.w = float_to_bf16_bits(dvacc[dt][4 * g + 3]);
+        a.x = Elt<T>::from_f(dkacc[dt][4 * g + 0] * P.scale);
+        a.y = Elt<T>::from_f(dkacc[dt][4 * g + 1] * P.scale);
+        a.z = Elt<T>::from_f(dkacc[dt][4 * g + 2] * P.scale);
+        a.w = Elt<T>::from_f(dkacc[dt][4 * g + 3] * P.scale);
+        c.x = Elt<T>::from_f(dvacc[dt][4 * g + 0]);
+        c.y = Elt<T>::from_f(dvacc[dt][4 * g + 1]);
+        c.z = Elt<T>::from_f(dvacc[dt][4 * g + 2]);
+        c.w = Elt<T>::from_f(dvacc[dt][4 * g + 3]);
         *reinterpret_cast<ushort4*>(dkp + dt * 32 + 8 * g + 4 * h) = a;
         *reinterpret_cast<ushort4*>(dvp + dt * 32 + 8 * g + 4 * h) = c;
       }
@@ -737,14 +753,14 @@ static void fa_launch(void (*kernel)(AttnParams), int grid, size_t smem, hipStre
 #define FA_DISPATCH_D(KERNEL, DD, causal, drop, kbias, grid, smem, st, P)         \
   do {                                                                          \
     if (causal) {                                                               \
-      if (drop) fa_launch(KERNEL<DD, true, true, false>, grid, smem, st, P);    \
-      else fa_launch(KERNEL<DD, true, false, false>, grid, smem, st, P);        \
+      if (drop) fa_launch(KERNEL<T, DD, true, true, false>, grid, smem, st, P); \
+      else fa_launch(KERNEL<T, DD, true, false, false>, grid, smem, st, P);     \
     } else if (kbias) {                                                         \
-      if (drop) fa_launch(KERNEL<DD, false, true, true>, grid, smem, st, P);    \
-      else fa_launch(KERNEL<DD, false, false, true>, grid, smem, st, P);        \
+      if (drop) fa_launch(KERNEL<T, DD, false, true, true>, grid, smem, st, P); \
+      else fa_launch(KERNEL<T, DD, false, false, true>, grid, smem, st, P);     \
     } else {                                                                    \
-      if (drop) fa_launch(KERNEL<DD, false, true, false>, grid, smem, st, P);   \
-      else fa_launch(KERNEL<DD, false, false, false>, grid, smem, st, P);       \
+      if (drop) fa_launch(KERNEL<T, DD, false, true, false>, grid, smem, st, P); \
+      else fa_launch(KERNEL<T, DD, false, false, false>, grid, smem, st, P);     \
     }                                                                           \
   } while (0)
 // key bias is only instantiated for non-causal attention (BERT-style padding
@@ -758,7 +774,8 @@ static void fa_launch(void (*kernel)(AttnParams), int grid, size_t smem, hipStre
 // strides arrays are {batch, seq, head} in elements; head dim contiguous.
 // kbias: optional [B, kb_stride] float additive key bias; kb_stride must be
 // >= round_up(Sk, 128) (tiles read whole 64-key groups).
-extern "C" int fx_flash_fwd(const void* q, const void* k, const void* v, void* out, float* lse,
+template <typename T>
+static int flash_fwd_t(const void* q, const void* k, const void* v, void* out, float* lse,
                             const long* qs, const long* ks, const long* vs, const long* os,
                             const int* kv_lens, const float* kbias, long kb_stride, int B, int H,
                             int Sq, int Sk, int D, int causal, float scale, float p, uint64_t key,
@@ -780,7 +797,8 @@ extern "C" int fx_flash_fwd(const void* q, const void* k, const void* v, void* o
 }
 
 // o/dout share strides `os`; dq uses `dqs`; dk/dv share `dks`.
-extern "C" int fx_flash_bwd(const void* q, const void* k, const void* v, const void* o,
+template <typename T>
+static int flash_bwd_t(const void* q, const void* k, const void* v, const void* o,
                             const void* dout, const float* lse, float* delta, void* dq, void* dk,
                             void* dv, const long* qs, const long* ks, const long* vs,
                             const long* os, const long* dqs, const long* dks, const int* kv_lens,
@@ -807,8 +825,8 @@ extern "C" int fx_flash_bwd(const void* q, const void* k, const void* v, const v
     const long rows = (long)B * H * Sq;
     const int rpb = 256 / (D / 8);
     const int grid = (int)((rows + rpb - 1) / rpb);
-    if (D == 128) fa_bwd_pre_kernel<128><<<grid, 256, 0, st>>>(P);
-    else fa_bwd_pre_kernel<64><<<grid, 256, 0, st>>>(P);
+    if (D == 128) fa_bwd_pre_kernel<T, 128><<<grid, 256, 0, st>>>(P);
+    else fa_bwd_pre_kernel<T, 64><<<grid, 256, 0, st>>>(P);
   }
   {
     const int nq = (Sq + 127) / 128;
@@ -823,4 +841,37 @@ extern "C" int fx_flash_bwd(const void* q, const void* k, const void* v, const v
                 P);
   }
   return 0;
+}
+
+// dt: 0 = bf16, 1 = fp16 (inputs, outputs and the MFMA operand type)
+extern "C" int fx_flash_fwd(int dt, const void* q, const void* k, const void* v, void* out,
+                            float* lse, const long* qs, const long* ks, const long* vs,
+                            const long* os, const int* kv_lens, const float* kbias,
+                            long kb_stride, int B, int H, int Sq, int Sk, int D, int causal,
+                            float scale, float p, uint64_t key, hipStream_t st) {
+  if (dt == 0)
+    return flash_fwd_t<bf16>(q, k, v, out, lse, qs, ks, vs, os, kv_lens, kbias, kb_stride, B, H,
+                             Sq, Sk, D, causal, scale, p, key, st);
+  if (dt == 1)
+    return flash_fwd_t<f16>(q, k, v, out, lse, qs, ks, vs, os, kv_lens, kbias, kb_stride, B, H,
+                            Sq, Sk, D, causal, scale, p, key, st);
+  return -3;
+}
+
+extern "C" int fx_flash_bwd(int dt, const void* q, const void* k, const void* v, const void* o,
+                            const void* dout, const float* lse, float* delta, void* dq, void* dk,
+                            void* dv, const long* qs, const long* ks, const long* vs,
+                            const long* os, const long* dqs, const long* dks, const int* kv_lens,
+                            const float* kbias, long kb_stride, int B, int H, int Sq, int Sk,
+                            int D, int causal, float scale, float p, uint64_t key,
+                            hipStream_t st) {
+  if (dt == 0)
+    return flash_bwd_t<bf16>(q, k, v, o, dout, lse, delta, dq, dk, dv, qs, ks, vs, os, dqs, dks,
+                             kv_lens, kbias, kb_stride, B, H, Sq, Sk, D, causal, scale, p, key,
+                             st);
+  if (dt == 1)
+    return flash_bwd_t<f16>(q, k, v, o, dout, lse, delta, dq, dk, dv, qs, ks, vs, os, dqs, dks,
+                            kv_lens, kbias, kb_stride, B, H, Sq, Sk, D, causal, scale, p, key,
+                            st);
+  return -3;
 }

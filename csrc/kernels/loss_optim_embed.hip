@@ -131,59 +131,84 @@ __global__ __launch_bounds__(256) void sumsq_f32_kernel(const float* __restrict_
 
 // --------------------------------------------------------------- AdamW
 // p (fp32 master), g (fp32), m, v (fp32); optional 16-bit model copy.
-// gscale: device scalar multiplied into g (clip coef / unscale); skip: device
-// int flag (found inf) -> no update.
+//  * gscale: device scalar multiplied into g (clip coefficient x 1/loss-scale);
+//  * skip: device int (fp16 found-inf) -> no update at all;
+//  * step: device int = number of APPLIED updates including this one (the
+//    optimizer advances it only when skip == 0, so an overflowed step does
+//    not advance Adam's bias corrections -- Paddle's beta_pow semantics);
+//  * wd: decoupled decay (AdamW); l2: classic L2 term added to the ALREADY
+//    clipped / unscaled gradient (Adam; Paddle applies regularisation after
+//    gradient clipping).
+// Streaming: 2 float4 groups per thread per iteration with every load issued
+// before any math (8 x 16-byte loads in flight per lane), non-temporal
+// accesses (each byte is touched once per step, keep it out of L2/MALL).
 template <typename T>
 __global__ __launch_bounds__(256) void adamw_flat_kernel(
     float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
     float* __restrict__ v, uint16_t* __restrict__ p16, long n, float lr, float beta1,
-    float beta2, float eps, float wd, float bc1, float bc2, const float* __restrict__ gscale,
-    const int* __restrict__ skip) {
+    float beta2, float eps, float wd, float l2, const float* __restrict__ gscale,
+    const int* __restrict__ skip, const int* __restrict__ step) {
   if (skip && *skip) return;
   const float gs = gscale ? *gscale : 1.f;
+  const float t = (float)(*step);
+  const float bc1 = 1.f - __powf(beta1, t);
+  const float bc2 = 1.f - __powf(beta2, t);
   const float step_size = lr / bc1;
   const float inv_sqrt_bc2 = rsqrtf(bc2);
+  const float decay = 1.f - lr * wd;
   const long n4 = n / 4;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    float4 pp = reinterpret_cast<float4*>(p)[i];
-    float4 gg = reinterpret_cast<const float4*>(g)[i];
-    float4 mm = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
-    float* pa = &pp.x;
-    float* ga = &gg.x;
-    float* ma = &mm.x;
-    float* va = &vv.x;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float gr = ga[j] * gs;
-      ma[j] = beta1 * ma[j] + (1.f - beta1) * gr;
-      va[j] = beta2 * va[j] + (1.f - beta2) * gr * gr;
-      float denom = sqrtf(va[j]) * inv_sqrt_bc2 + eps;
-      pa[j] = pa[j] * (1.f - lr * wd) - step_size * ma[j] / denom;
+  const long stride = (long)gridDim.x * 512;
+  for (long i0 = blockIdx.x * 512L + threadIdx.x; i0 < n4; i0 += stride) {
+    const long i1 = i0 + 256;
+    const bool two = i1 < n4;
+    floatx4 pp[2], gg[2], mm[2], vv[2];
+    pp[0] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(p) + i0);
+    gg[0] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(g) + i0);
+    mm[0] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(m) + i0);
+    vv[0] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(v) + i0);
+    if (two) {
+      pp[1] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(p) + i1);
+      gg[1] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(g) + i1);
+      mm[1] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(m) + i1);
+      vv[1] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(v) + i1);
     }
-    reinterpret_cast<float4*>(p)[i] = pp;
-    reinterpret_cast<float4*>(m)[i] = mm;
-    reinterpret_cast<float4*>(v)[i] = vv;
-    if (p16) {
-      ushort4 o;
-      o.x = Elt<T>::from_f(pa[0]);
-      o.y = Elt<T>::from_f(pa[1]);
-      o.z = Elt<T>::from_f(pa[2]);
-      o.w = Elt<T>::from_f(pa[3]);
-      reinterpret_cast<ushort4*>(p16)[i] = o;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !two) break;
+      const long i = u ? i1 : i0;
+      floatx4 pa = pp[u], ma = mm[u], va = vv[u];
+      const floatx4 ga = gg[u];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float gr = ga[j] * gs + l2 * pa[j];
+        ma[j] = beta1 * ma[j] + (1.f - beta1) * gr;
+        va[j] = beta2 * va[j] + (1.f - beta2) * gr * gr;
+        const float denom = sqrtf(va[j]) * inv_sqrt_bc2 + eps;
+        pa[j] = pa[j] * decay - step_size * ma[j] / denom;
+      }
+      __builtin_nontemporal_store(pa, reinterpret_cast<floatx4*>(p) + i);
+      __builtin_nontemporal_store(ma, reinterpret_cast<floatx4*>(m) + i);
+      __builtin_nontemporal_store(va, reinterpret_cast<floatx4*>(v) + i);
+      if (p16) {
+        ushort4 o;
+        o.x = Elt<T>::from_f(pa[0]);
+        o.y = Elt<T>::from_f(pa[1]);
+        o.z = Elt<T>::from_f(pa[2]);
+        o.w = Elt<T>::from_f(pa[3]);
+        reinterpret_cast<ushort4*>(p16)[i] = o;
+      }
     }
   }
   for (long i = n4 * 4 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    float gr = g[i] * gs;
+    const float gr = g[i] * gs + l2 * p[i];
     m[i] = beta1 * m[i] + (1.f - beta1) * gr;
     v[i] = beta2 * v[i] + (1.f - beta2) * gr * gr;
-    float denom = sqrtf(v[i]) * inv_sqrt_bc2 + eps;
-    p[i] = p[i] * (1.f - lr * wd) - step_size * m[i] / denom;
+    const float denom = sqrtf(v[i]) * inv_sqrt_bc2 + eps;
+    p[i] = p[i] * decay - step_size * m[i] / denom;
     if (p16) p16[i] = Elt<T>::from_f(p[i]);
   }
 }
 
-// copy fp32 -> 16-bit (param refresh after all-gather / load)
 template <typename T>
 __global__ __launch_bounds__(256) void cast_f32_kernel(const float* __restrict__ x,
                                                        uint16_t* __restrict__ y, long n) {
@@ -326,12 +351,15 @@ extern "C" void fx_sumsq_f32(const float* x, long n, float* partial, int blocks,
 
 extern "C" void fx_adamw_flat(int dtype, float* p, const float* g, float* m, float* v, void* p16,
                               long n, float lr, float beta1, float beta2, float eps, float wd,
-                              float bc1, float bc2, const float* gscale, const int* skip,
+                              float l2, const float* gscale, const int* skip, const int* step,
                               hipStream_t st) {
-  int grid = grid_n(n / 4 + 1, 256);
+  // two float4 groups per thread per pass; at most 8 resident 256-thread blocks per CU
+  long blocks = (n / 4 + 511) / 512;
+  const long cap = 256L * 8 * 4;
+  int grid = (int)(blocks < 1 ? 1 : (blocks > cap ? cap : blocks));
   FX_DISPATCH_T(dtype, adamw_flat_kernel<T><<<grid, 256, 0, st>>>(
-                           p, g, m, v, (uint16_t*)p16, n, lr, beta1, beta2, eps, wd, bc1, bc2,
-                           gscale, skip));
+                           p, g, m, v, (uint16_t*)p16, n, lr, beta1, beta2, eps, wd, l2,
+                           gscale, skip, step));
 }
 
 extern "C" void fx_cast_f32(int dtype, const float* x, void* y, long n, hipStream_t st) {

@@ -6,10 +6,8 @@
 // K18/K19 (generation decode with a KV cache, `single_model.py:109-114`,
 // Paddle fused_multi_transformer decode path).
 //
-// Decode attention is memory bound (one query row per (batch, head)): one
-// workgroup per (batch, head), 16 lanes x 16 bytes cover a D=128 key row, so a
-// wave scores 4 keys per step; online softmax per lane group, merged through
-// LDS at the end.
+// Decode attention is memory bound (one query row per (batch, head)): split-K
+// over the cached keys (see decode_attn_split_kernel).
 #include "fx_common.h"
 
 namespace {
@@ -53,51 +51,84 @@ __global__ __launch_bounds__(256) void fake_quant_kernel(const uint16_t* __restr
   }
 }
 
+// Split-K ("flash-decoding") single-token attention over a KV cache.
 // q: [B, H, D] (strides sqb, sqh); caches: [B, maxlen, H, D] (skb, sks, skh);
-// out: [B, H, D] (sob, D contiguous, head stride D)
-template <int D>
-__global__ __launch_bounds__(256) void decode_attn_kernel(
+// out: [B, H, D] (sob, D contiguous, head stride D).
+// Pass 1: grid = B*H*nsplit workgroups; split s of (b, h) scores keys
+//   [s*chunk, min((s+1)*chunk, len)): D/8 lanes cover one key row with 16-byte
+//   loads, each lane group keeps 4 keys in flight per step (the kernel is HBM
+//   bound: every cached byte is read once), online softmax per lane group,
+//   merged through LDS into one partial (m, l, o[D]) per workgroup.
+// Pass 2: one workgroup per (b, h) merges the nsplit partials.
+// Small-batch long-context decode thus spreads over B*H*nsplit >= ~2 waves of
+// workgroups instead of B*H (a few CUs out of 256).
+template <typename T, int D>
+__global__ __launch_bounds__(256) void decode_attn_split_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
-    const uint16_t* __restrict__ vc, uint16_t* __restrict__ out, const int* __restrict__ lens,
-    int H, long sqb, long sqh, long skb, long sks, long skh, long sob, float scale) {
+    const uint16_t* __restrict__ vc, const int* __restrict__ lens, float* __restrict__ ws,
+    int H, int nsplit, int chunk, long sqb, long sqh, long skb, long sks, long skh, float scale) {
   constexpr int LPK = D / 8;        // lanes per key row
-  constexpr int KPW = 64 / LPK;     // keys per wave step
-  const int bh = blockIdx.x, b = bh / H, hd = bh % H;
+  constexpr int KPW = 64 / LPK;     // key rows per wave instruction
+  constexpr int U = 4;              // key rows per lane group per step
+  const int split = blockIdx.x % nsplit, bh = blockIdx.x / nsplit;
+  const int b = bh / H, hd = bh % H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int sub = lane / LPK, c = (lane % LPK) * 8;
   const int len = lens[b];
+  const int k_lo = split * chunk, k_hi = min(len, k_lo + chunk);
   float qv[8];
-  load8<bf16>(q + b * sqb + hd * sqh + c, qv);
+  load8<T>(q + b * sqb + hd * sqh + c, qv);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) qv[j] *= scale;
   float m = -INFINITY, l = 0.f, o[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) o[j] = 0.f;
   const uint16_t* kb = kc + b * skb + hd * skh + c;
   const uint16_t* vb = vc + b * skb + hd * skh + c;
-  for (int k0 = w * KPW; k0 < len; k0 += 4 * KPW) {
-    const int key = k0 + sub;
-    float kv[8], s = 0.f;
-    const bool valid = key < len;
-    if (valid) {
-      load8<bf16>(kb + (long)key * sks, kv);
+  // wave w, step: keys k0 + u*KPW*4 + w*KPW + sub, u < U
+  for (int k0 = k_lo; k0 < k_hi; k0 += 4 * KPW * U) {
+    float sc[U];
+    int key[U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += kv[j] * qv[j];
+    for (int u = 0; u < U; ++u) {
+      key[u] = k0 + (u * 4 + w) * KPW + sub;
+      float kv[8];
+      sc[u] = 0.f;
+      if (key[u] < k_hi) {
+        load8<T>(kb + (long)key[u] * sks, kv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sc[u] += kv[j] * qv[j];
+      }
     }
 #pragma unroll
-    for (int off = LPK / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-    s = valid ? s * scale : -INFINITY;
-    if (valid) {
-      const float mn = fmaxf(m, s);
-      const float a = __expf(m - mn), p = __expf(s - mn);
+    for (int off = LPK / 2; off > 0; off >>= 1)
+#pragma unroll
+      for (int u = 0; u < U; ++u) sc[u] += __shfl_xor(sc[u], off, 64);
+    float mx = m;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (key[u] >= k_hi) sc[u] = -INFINITY;
+      mx = fmaxf(mx, sc[u]);
+    }
+    if (mx == -INFINITY) continue;
+    const float a = __expf(m - mx);
+    l *= a;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] *= a;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (key[u] >= k_hi) continue;
+      const float p = __expf(sc[u] - mx);
       float vv[8];
-      load8<bf16>(vb + (long)key * sks, vv);
+      load8<T>(vb + (long)key[u] * sks, vv);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = o[j] * a + p * vv[j];
-      l = l * a + p;
-      m = mn;
+      for (int j = 0; j < 8; ++j) o[j] += p * vv[j];
+      l += p;
     }
+    m = mx;
   }
-  // merge the KPW*4 partial states of each column slice through LDS
-  __shared__ float sm_m[4 * 64], sm_l[4 * 64], sm_o[4 * 64][8];
+  // merge the 4*KPW lane-group states of each column slice through LDS
+  __shared__ float sm_m[256], sm_l[256], sm_o[256][8];
   sm_m[threadIdx.x] = m;
   sm_l[threadIdx.x] = l;
 #pragma unroll
@@ -109,18 +140,44 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
     float L = 0.f, O[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) O[j] = 0.f;
-    for (int t = threadIdx.x; t < 256; t += LPK) {
-      if (sm_m[t] == -INFINITY) continue;
-      const float a = __expf(sm_m[t] - M);
-      L += sm_l[t] * a;
+    if (M != -INFINITY) {
+      for (int t = threadIdx.x; t < 256; t += LPK) {
+        if (sm_m[t] == -INFINITY) continue;
+        const float a = __expf(sm_m[t] - M);
+        L += sm_l[t] * a;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) O[j] += sm_o[t][j] * a;
+        for (int j = 0; j < 8; ++j) O[j] += sm_o[t][j] * a;
+      }
     }
-    const float inv = L > 0.f ? 1.f / L : 0.f;
+    float* wp = ws + (long)blockIdx.x * (D + 2);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) O[j] *= inv;
-    store8<bf16>(out + b * sob + hd * D + threadIdx.x * 8, O);
+    for (int j = 0; j < 8; ++j) wp[threadIdx.x * 8 + j] = O[j];
+    if (threadIdx.x == 0) {
+      wp[D] = M;
+      wp[D + 1] = L;
+    }
   }
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(D) void decode_attn_combine_kernel(const float* __restrict__ ws,
+                                                               uint16_t* __restrict__ out, int H,
+                                                               int nsplit, long sob) {
+  const int bh = blockIdx.x, b = bh / H, hd = bh % H, d = threadIdx.x;
+  const float* base = ws + (long)bh * nsplit * (D + 2);
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, base[s * (D + 2) + D]);
+  float L = 0.f, O = 0.f;
+  if (M != -INFINITY) {
+    for (int s = 0; s < nsplit; ++s) {
+      const float* wp = base + s * (D + 2);
+      if (wp[D] == -INFINITY) continue;
+      const float a = __expf(wp[D] - M);
+      L += wp[D + 1] * a;
+      O += wp[d] * a;
+    }
+  }
+  out[b * sob + hd * D + d] = Elt<T>::from_f(L > 0.f ? O / L : 0.f);
 }
 
 }  // namespace
@@ -145,21 +202,29 @@ extern "C" int fx_fake_quant_fwd(int dtype, const void* x, void* y, const float*
   return 0;
 }
 
-extern "C" int fx_decode_attn(const void* q, const void* kc, const void* vc, void* out,
+// dt: 0 bf16 / 1 fp16; ws: fp32 workspace of B*H*nsplit*(D+2); chunk = keys per split
+extern "C" int fx_decode_attn(int dt, const void* q, const void* kc, const void* vc, void* out,
                               const int* lens, int B, int H, int D, int maxlen, int nsplit,
-                              long sqb, long sqh, long skb, long sks, long skh, long sob,
-                              float scale, hipStream_t st) {
-  (void)maxlen;
-  (void)nsplit;
-  if (D == 128)
-    decode_attn_kernel<128><<<B * H, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)kc,
-                                                  (const uint16_t*)vc, (uint16_t*)out, lens, H,
-                                                  sqb, sqh, skb, sks, skh, sob, scale);
-  else if (D == 64)
-    decode_attn_kernel<64><<<B * H, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)kc,
-                                                 (const uint16_t*)vc, (uint16_t*)out, lens, H, sqb,
-                                                 sqh, skb, sks, skh, sob, scale);
-  else
-    return -1;
+                              float* ws, long sqb, long sqh, long skb, long sks, long skh,
+                              long sob, float scale, hipStream_t st) {
+  if (D != 64 && D != 128) return -1;
+  if (nsplit < 1) return -2;
+  const int chunk = (maxlen + nsplit - 1) / nsplit;
+  const int g = B * H * nsplit;
+#define FX_DEC(TT, DD)                                                                           \
+  do {                                                                                           \
+    decode_attn_split_kernel<TT, DD><<<g, 256, 0, st>>>(                                         \
+        (const uint16_t*)q, (const uint16_t*)kc, (const uint16_t*)vc, lens, ws, H, nsplit, chunk, \
+        sqb, sqh, skb, sks, skh, scale);                                                         \
+    decode_attn_combine_kernel<TT, DD><<<B * H, DD, 0, st>>>(ws, (uint16_t*)out, H, nsplit, sob); \
+  } while (0)
+  if (dt == 0) {
+    if (D == 128) FX_DEC(bf16, 128); else FX_DEC(bf16, 64);
+  } else if (dt == 1) {
+    if (D == 128) FX_DEC(f16, 128); else FX_DEC(f16, 64);
+  } else {
+    return -3;
+  }
+#undef FX_DEC
   return 0;
 }

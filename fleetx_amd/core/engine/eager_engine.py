@@ -44,28 +44,40 @@ _END = object()
 
 
 class DynamicLossScaler:
-    """Device-resident GradScaler (reference K14; ``eager_engine.py:157-167``)."""
+    """Device-resident GradScaler (reference K14; ``eager_engine.py:157-167``).
+
+    Paddle ``GradScaler`` semantics: the scale is multiplied by ``decr_ratio``
+    only after ``decr_every_n_nan_or_inf`` CONSECUTIVE overflowing steps, and by
+    ``incr_ratio`` after ``incr_every_n_steps`` consecutive finite ones."""
 
     def __init__(self, init_scale=32768.0, incr_every=1000, incr_ratio=2.0, decr_ratio=0.5,
-                 device="cpu"):
+                 decr_every=2, device="cpu"):
         self.scale = torch.full((), float(init_scale), dtype=torch.float32, device=device)
         self.good = torch.zeros((), dtype=torch.int32, device=device)
+        self.bad = torch.zeros((), dtype=torch.int32, device=device)
         self.incr_every, self.incr_ratio, self.decr_ratio = incr_every, incr_ratio, decr_ratio
+        self.decr_every = int(decr_every)
 
     def update(self, found_inf):
         inf = found_inf.reshape(()).bool()
-        self.good = torch.where(inf, torch.zeros_like(self.good), self.good + 1)
+        zero = torch.zeros_like(self.good)
+        self.good = torch.where(inf, zero, self.good + 1)
+        self.bad = torch.where(inf, self.bad + 1, zero)
         grow = self.good >= self.incr_every
-        self.scale = torch.where(inf, self.scale * self.decr_ratio,
+        shrink = self.bad >= self.decr_every
+        self.scale = torch.where(shrink, self.scale * self.decr_ratio,
                                  torch.where(grow, self.scale * self.incr_ratio, self.scale))
-        self.good = torch.where(grow, torch.zeros_like(self.good), self.good)
+        self.good = torch.where(grow, zero, self.good)
+        self.bad = torch.where(shrink, zero, self.bad)
 
     def state_dict(self):
-        return {"scale": self.scale.cpu(), "good": self.good.cpu()}
+        return {"scale": self.scale.cpu(), "good": self.good.cpu(), "bad": self.bad.cpu()}
 
     def load_state_dict(self, s):
         self.scale.copy_(s["scale"])
         self.good.copy_(s["good"])
+        if "bad" in s:
+            self.bad.copy_(s["bad"])
 
 
 def _to_device(batch, device):
@@ -174,7 +186,13 @@ class EagerEngine(BasicEngine):
                                              pp_group=self.hcg.get_pipe_parallel_group(),
                                              offload=bool(sh.get("sharding_offload", False)))
             if self._use_pure_fp16 and self._dtype == torch.float16:
-                self.scaler = DynamicLossScaler(amp.get("scale_loss", 32768.0), device=self.device)
+                self.scaler = DynamicLossScaler(
+                    amp.get("scale_loss", 32768.0),
+                    incr_every=int(amp.get("incr_every_n_steps", 1000)),
+                    incr_ratio=float(amp.get("incr_ratio", 2.0)),
+                    decr_ratio=float(amp.get("decr_ratio", 0.5)),
+                    decr_every=int(amp.get("decr_every_n_nan_or_inf", 2)),
+                    device=self.device)
                 self.optimizer.loss_scale = self.scaler.scale
             # step N's AdamW runs on a side stream under step N+1's forward
             if comm.get("overlap_optimizer", True) and not self._pipeline \
@@ -484,7 +502,16 @@ class EagerEngine(BasicEngine):
             raise FileNotFoundError("{} not found".format(mp))
         sd = ckpt.load_payload(mp)
         with self._params_gathered(writeback=True):
-            self._module.model.load_state_dict(sd, strict=False)
+            res = self._module.model.load_state_dict(sd, strict=False)
+        missing = [k for k in res.missing_keys
+                   if dict(self._module.model.named_parameters()).get(k) is not None
+                   and dict(self._module.model.named_parameters())[k].requires_grad]
+        if missing:
+            raise RuntimeError("checkpoint {} lacks {} trainable parameter(s) of this model, e.g. "
+                               "{}".format(mp, len(missing), missing[:5]))
+        if res.unexpected_keys:
+            logger.warning("checkpoint {}: {} unexpected key(s) ignored, e.g. {}".format(
+                mp, len(res.unexpected_keys), res.unexpected_keys[:5]))
         if self.mode == "train":
             op, mt = os.path.join(d, "model_state.pdopt"), os.path.join(d, "meta_state.pdopt")
             if not (os.path.isfile(op) and os.path.isfile(mt)):

@@ -73,11 +73,25 @@ def _visible_device_count():
         v = os.environ.get(var)
         if v is not None:
             return len([x for x in v.split(",") if x.strip()])
-    try:  # counting devices does not initialise the GPU
-        import torch
-        return torch.cuda.device_count()
-    except Exception:  # pragma: no cover - torch always importable here
+    # Count GPUs from the KFD topology in sysfs (nodes with SIMDs are GPUs):
+    # the watcher process never loads the HIP runtime (it forks the ranks and
+    # outlives them).
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        for node in os.listdir(root):
+            try:
+                with open(os.path.join(root, node, "properties")) as f:
+                    for line in f:
+                        k, _, v = line.partition(" ")
+                        if k == "simd_count" and int(v) > 0:
+                            n += 1
+                            break
+            except (OSError, ValueError):
+                continue
+    except OSError:
         return 0
+    return n
 
 
 def device_list(args):

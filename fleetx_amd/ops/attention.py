@@ -67,12 +67,16 @@ class _FlashAttn(torch.autograd.Function):
         for t in (q, k, v):
             if t.stride(-1) != 1:
                 raise ValueError("head dim must be contiguous")
+            if t.dtype != q.dtype:
+                raise TypeError("flash attention: q/k/v dtypes differ ({}, {})".format(q.dtype, t.dtype))
+        dt = _lib.dt_code(q.dtype)  # bf16 / fp16 kernels; anything else raises
+        ctx.dt = dt
         k_ = _lib.kernels()
         out = torch.empty(B, Sq, H, D, device=q.device, dtype=q.dtype)
         lse = torch.empty(B * H * Sq, device=q.device, dtype=torch.float32)
         kl = kv_lens.to(torch.int32).contiguous() if kv_lens is not None else None
         kb = _padded_bias(key_bias, B, Sk, q.device)
-        rc = k_.flash_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), lse.data_ptr(),
+        rc = k_.flash_fwd(dt, q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), lse.data_ptr(),
                           _strides(q), _strides(k), _strides(v), _strides(out), _lib.ptr(kl),
                           _lib.ptr(kb), kb.shape[1] if kb is not None else 0,
                           B, H, Sq, Sk, D, int(causal), float(scale), float(p), key,
@@ -100,7 +104,7 @@ class _FlashAttn(torch.autograd.Function):
             dv = torch.empty_like(dk)
         delta = torch.empty(B * H * Sq, device=q.device, dtype=torch.float32)
         rc = _lib.kernels().flash_bwd(
-            q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), dout.data_ptr(),
+            ctx.dt, q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), dout.data_ptr(),
             lse.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
             _strides(q), _strides(k), _strides(v), _strides(out), _strides(dq), _strides(dk),
             _lib.ptr(kl), _lib.ptr(kb), kb.shape[1] if kb is not None else 0,
@@ -214,8 +218,15 @@ def flash_attention_qkvpacked(qkv, causal=True, dropout_p=0.0, key=0, scale=None
     return _PackedEntry.apply(qkv, causal, float(dropout_p), key, scale, kv_lens, key_bias)
 
 
-def decode_attention(q, k_cache, v_cache, lens, scale=None):
-    """Single-token attention over a KV cache.
+def decode_splits(B, H, maxlen, target_wgs=512, min_chunk=128):
+    """Split-K factor for decode attention: enough workgroups to cover the 256
+    CUs about twice, at least ``min_chunk`` keys per split."""
+    n = max(1, -(-target_wgs // max(1, B * H)))
+    return max(1, min(n, -(-maxlen // min_chunk)))
+
+
+def decode_attention(q, k_cache, v_cache, lens, scale=None, nsplit=None):
+    """Single-token attention over a KV cache (split-K, bf16 / fp16).
 
     q: [B, H, D]; caches: [B, maxlen, H, D]; lens: int32 [B] valid lengths.
     """
@@ -227,12 +238,20 @@ def decode_attention(q, k_cache, v_cache, lens, scale=None):
         m = torch.arange(L, device=q.device).view(1, 1, L) >= lens.view(B, 1, 1).to(q.device)
         p = torch.softmax(s.masked_fill(m, float("-inf")), -1)
         return torch.einsum("bhl,blhd->bhd", p, v_cache.float()).to(q.dtype)
+    dt = _lib.dt_code(q.dtype)
+    if k_cache.dtype != q.dtype or v_cache.dtype != q.dtype:
+        raise TypeError("decode attention: q / cache dtypes differ")
+    if k_cache.stride() != v_cache.stride() or k_cache.stride(-1) != 1 or q.stride(-1) != 1:
+        raise ValueError("decode attention: caches must share a layout with contiguous head dim")
+    maxlen = k_cache.shape[1]
+    ns = nsplit or decode_splits(B, H, maxlen)
     out = torch.empty(B, H, D, device=q.device, dtype=q.dtype)
-    rc = _lib.kernels().decode_attn(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+    ws = torch.empty(B * H * ns * (D + 2), device=q.device, dtype=torch.float32)
+    rc = _lib.kernels().decode_attn(dt, q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                     out.data_ptr(), lens.to(torch.int32).contiguous().data_ptr(),
-                                    B, H, D, k_cache.shape[1], 1, q.stride(0), q.stride(1),
+                                    B, H, D, maxlen, ns, ws.data_ptr(), q.stride(0), q.stride(1),
                                     k_cache.stride(0), k_cache.stride(1), k_cache.stride(2),
                                     out.stride(0), float(scale), _lib.stream())
     if rc != 0:
-        raise NotImplementedError("decode attention supports head_dim 64/128")
+        raise NotImplementedError("decode attention supports head_dim 64/128 (rc %d)" % rc)
     return out

@@ -74,6 +74,10 @@ class FlatOptimizer:
         else:
             self.master = [buffer.param_flat[s:e].float().clone() for s, e, _ in self.ranges]
         self.found_inf = torch.zeros(1, dtype=torch.int32, device=dev)
+        # number of APPLIED updates (advanced on the device only when found_inf
+        # is 0): Adam's bias corrections follow it, so fp16 overflow steps do
+        # not age the moments (Paddle's beta_pow semantics)
+        self.dev_step = torch.zeros(1, dtype=torch.int32, device=dev)
         self.gscale = torch.ones(1, dtype=torch.float32, device=dev)
         self.last_grad_norm = torch.zeros((), dtype=torch.float32, device=dev)
         self.loss_scale = None  # set by the engine for fp16 (device tensor)
@@ -147,6 +151,7 @@ class FlatOptimizer:
             sync()
         self._prepare_scale()
         self.step_count += 1
+        self.dev_step.add_(1 - self.found_inf)
         self._update(self.get_lr())
         self.buffer.allgather_params()
 
@@ -263,7 +268,7 @@ class FusedAdamW(FlatOptimizer):
             self.m = [torch.zeros_like(x) for x in self.master]
             self.v = [torch.zeros_like(x) for x in self.master]
 
-    def _update_overlapped(self, lr, bc1, bc2):
+    def _update_overlapped(self, lr):
         """AdamW per unit (root first, then layer 0, 1, ...) on the side
         stream; an event per unit gates that unit's next forward."""
         k = _lib.kernels()
@@ -282,13 +287,13 @@ class FusedAdamW(FlatOptimizer):
                     k.adamw_flat(dt, self.master[ri][a:b].data_ptr(), gf[lo:hi].data_ptr(),
                                  self.m[ri][a:b].data_ptr(), self.v[ri][a:b].data_ptr(),
                                  pf[lo:hi].data_ptr(), hi - lo, float(lr), self.beta1, self.beta2,
-                                 self.eps, float(wd), bc1, bc2, self.gscale.data_ptr(),
-                                 self.found_inf.data_ptr(), st)
+                                 self.eps, float(wd), 0.0, self.gscale.data_ptr(),
+                                 self.found_inf.data_ptr(), self.dev_step.data_ptr(), st)
                 ev = torch.cuda.Event()
                 ev.record(os_)
                 self._unit_events[u] = ev
 
-    def _update_offloaded(self, lr, bc1, bc2):
+    def _update_offloaded(self, lr):
         """Stream host-resident master/m/v through the GPU in chunks: the H2D
         copy of chunk j+1 and the D2H copy of chunk j-1 run on a copy stream
         while the fused AdamW kernel updates chunk j (reference
@@ -323,8 +328,9 @@ class FusedAdamW(FlatOptimizer):
             cur.wait_event(ready)
             k.adamw_flat(_lib.dt_code(pf.dtype), st[0].data_ptr(), gviews[ri][o:o + n].data_ptr(),
                          st[1].data_ptr(), st[2].data_ptr(), pf[s + o:s + o + n].data_ptr(), n,
-                         float(lr), self.beta1, self.beta2, self.eps, float(wd), bc1, bc2,
-                         self.gscale.data_ptr(), self.found_inf.data_ptr(), _lib.stream())
+                         float(lr), self.beta1, self.beta2, self.eps, float(wd), 0.0,
+                         self.gscale.data_ptr(), self.found_inf.data_ptr(),
+                         self.dev_step.data_ptr(), _lib.stream())
             done = torch.cuda.Event()
             done.record(cur)
             with torch.cuda.stream(cs):
@@ -334,51 +340,52 @@ class FusedAdamW(FlatOptimizer):
             ready = nxt
 
     def _update(self, lr):
-        t = self.step_count
-        bc1 = 1.0 - self.beta1 ** t
-        bc2 = 1.0 - self.beta2 ** t
         if self.offload:
             if not self.decoupled:
                 raise NotImplementedError("sharding_offload supports the decoupled AdamW family")
-            return self._update_offloaded(lr, bc1, bc2)
+            return self._update_offloaded(lr)
         if self._overlap_groups is not None and self.decoupled:
-            return self._update_overlapped(lr, bc1, bc2)
+            return self._update_overlapped(lr)
         pf = self.buffer.param_flat
         for (s, e, c), g, p, m, v in zip(self.ranges, self.grad_views(), self.master, self.m,
                                          self.v):
             wd = self.weight_decay if c.decay else 0.0
-            if not self.decoupled and wd:
-                g = g + wd * p
-                wd_eff = 0.0
-            else:
-                wd_eff = wd
+            # AdamW: decoupled decay on the weights; Adam: L2 term added to the
+            # gradient AFTER clipping / loss-scale unscaling
+            wd_dec, l2 = (wd, 0.0) if self.decoupled else (0.0, wd)
             out16 = pf[s:e]
             if p.is_cuda:
                 _lib.kernels().adamw_flat(_lib.dt_code(pf.dtype), p.data_ptr(), g.data_ptr(),
                                           m.data_ptr(), v.data_ptr(), out16.data_ptr(), p.numel(),
                                           float(lr), self.beta1, self.beta2, self.eps,
-                                          float(wd_eff), bc1, bc2, self.gscale.data_ptr(),
-                                          self.found_inf.data_ptr(), _lib.stream())
+                                          float(wd_dec), float(l2), self.gscale.data_ptr(),
+                                          self.found_inf.data_ptr(), self.dev_step.data_ptr(),
+                                          _lib.stream())
             else:
                 if int(self.found_inf.item()):
                     continue
-                gg = g * self.gscale
+                t = int(self.dev_step.item())
+                bc1 = 1.0 - self.beta1 ** t
+                bc2 = 1.0 - self.beta2 ** t
+                gg = g * self.gscale + l2 * p
                 m.mul_(self.beta1).add_(gg, alpha=1 - self.beta1)
                 v.mul_(self.beta2).addcmul_(gg, gg, value=1 - self.beta2)
                 denom = v.sqrt() / math.sqrt(bc2) + self.eps
-                p.mul_(1 - lr * wd_eff).addcdiv_(m, denom, value=-lr / bc1)
+                p.mul_(1 - lr * wd_dec).addcdiv_(m, denom, value=-lr / bc1)
                 out16.copy_(p)
 
     def state_dict(self):
         self.sync_state()
         cp = (lambda x: x.clone()) if self.offload else (lambda x: x.cpu())
-        return {"step": self.step_count, "master": [cp(x) for x in self.master],
+        return {"step": self.step_count, "applied_step": int(self.dev_step.item()),
+                "master": [cp(x) for x in self.master],
                 "m": [cp(x) for x in self.m], "v": [cp(x) for x in self.v],
                 "lr": self._lr.state_dict() if hasattr(self._lr, "state_dict") else self._lr}
 
     def set_state_dict(self, state):
         self.sync_state()
         self.step_count = state["step"]
+        self.dev_step.fill_(int(state.get("applied_step", state["step"])))
         for dst, src in zip(self.master, state["master"]):
             dst.copy_(src)
         for dst, src in zip(self.m, state["m"]):

@@ -191,16 +191,41 @@ def test_flash_attention_tail_and_kvlens():
         assert _rel(a.grad, r.grad) < 3e-2
 
 
-def test_decode_attention():
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("nsplit", [1, None, 7])
+def test_decode_attention(dtype, D, nsplit):
+    """Split-K decode vs fp32: ragged lengths, splits that end up empty."""
     from fleetx_amd import ops
-    B, H, D, L = 3, 4, 128, 300
-    q = torch.randn(B, H, D, device=DEV, dtype=torch.bfloat16)
-    kc = torch.randn(B, L, H, D, device=DEV, dtype=torch.bfloat16)
-    vc = torch.randn(B, L, H, D, device=DEV, dtype=torch.bfloat16)
-    lens = torch.tensor([300, 17, 128], device=DEV, dtype=torch.int32)
-    out = ops.decode_attention(q, kc, vc, lens)
+    B, H, L = 3, 4, 1300
+    q = torch.randn(B, H, D, device=DEV, dtype=dtype)
+    kc = torch.randn(B, L, H, D, device=DEV, dtype=dtype)
+    vc = torch.randn(B, L, H, D, device=DEV, dtype=dtype)
+    lens = torch.tensor([1300, 17, 700], device=DEV, dtype=torch.int32)
+    out = ops.decode_attention(q, kc, vc, lens, nsplit=nsplit)
+    assert out.dtype == dtype
     ref = ops.decode_attention(q.cpu().float(), kc.cpu().float(), vc.cpu().float(), lens.cpu())
     assert _rel(out.cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_fp16(D, causal):
+    """fp16 flash forward + backward (f16 MFMA path) vs fp32."""
+    from fleetx_amd import ops
+    B, S, H = 2, 320, 4
+    qkv = (0.5 * torch.randn(B, S, H, 3, D, device=DEV)).half().requires_grad_()
+    out = ops.flash_attention_qkvpacked(qkv, causal=causal)
+    assert out.dtype == torch.float16
+    ref_in = qkv.detach().float().requires_grad_()
+    ref = ops.attention_reference(ref_in[:, :, :, 0], ref_in[:, :, :, 1], ref_in[:, :, :, 2],
+                                  causal=causal)
+    assert _rel(out, ref) < 5e-3, _rel(out, ref)
+    g = torch.randn_like(ref)
+    out.backward(g.half())
+    ref.backward(g)
+    for i in range(3):
+        assert _rel(qkv.grad[:, :, :, i], ref_in.grad[:, :, :, i]) < 1e-2
 
 
 # ---------------------------------------------------------------- optimizer

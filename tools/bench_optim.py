@@ -1,0 +1,54 @@
+"""Bandwidth of the fused AdamW kernel (csrc/kernels/loss_optim_embed.hip) in
+isolation: 30 B per parameter (fp32 p/g/m/v in, p/m/v + bf16 copy out).
+
+    python tools/bench_optim.py [--n 1e9 --iters 10]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), "..")))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=float, default=1e9)
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    from fleetx_amd.ops import _lib
+    k = _lib.kernels()
+    n = int(a.n)
+    dev = "cuda"
+    p = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev) * 1e-3
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    p16 = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    gs = torch.ones(1, device=dev)
+    skip = torch.zeros(1, device=dev, dtype=torch.int32)
+    step = torch.ones(1, device=dev, dtype=torch.int32)
+
+    def run():
+        k.adamw_flat(0, p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p16.data_ptr(), n,
+                     1e-4, 0.9, 0.95, 1e-8, 0.01, 0.0, gs.data_ptr(), skip.data_ptr(),
+                     step.data_ptr(), _lib.stream())
+    for _ in range(2):
+        run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.iters):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / a.iters
+    print(json.dumps({"kernel": "adamw_flat", "n": n, "ms": round(ms, 3),
+                      "TB_s": round(30.0 * n / ms / 1e9, 3),
+                      "ms_per_6.65B_params": round(ms * 6.65e9 / n, 2)}))
+
+
+if __name__ == "__main__":
+    main()
