@@ -142,7 +142,16 @@ __global__ __launch_bounds__(256) void sumsq_f32_kernel(const float* __restrict_
 // Streaming: 2 float4 groups per thread per iteration with every load issued
 // before any math (8 x 16-byte loads in flight per lane), non-temporal
 // accesses (each byte is touched once per step, keep it out of L2/MALL).
-template <typename T>
+template <typename V>
+__device__ __forceinline__ V ld_stream(const V* a, bool nt) {
+  return nt ? __builtin_nontemporal_load(a) : *a;
+}
+template <typename V>
+__device__ __forceinline__ void st_stream(V x, V* a, bool nt) {
+  if (nt) __builtin_nontemporal_store(x, a); else *a = x;
+}
+
+template <typename T, bool NT>
 __global__ __launch_bounds__(256) void adamw_flat_kernel(
     float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
     float* __restrict__ v, uint16_t* __restrict__ p16, long n, float lr, float beta1,
@@ -162,15 +171,15 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(
     const long i1 = i0 + 256;
     const bool two = i1 < n4;
     floatx4 pp[2], gg[2], mm[2], vv[2];
-    pp[0] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(p) + i0);
-    gg[0] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(g) + i0);
-    mm[0] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(m) + i0);
-    vv[0] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(v) + i0);
+    pp[0] = ld_stream(reinterpret_cast<const floatx4*>(p) + i0, NT);
+    gg[0] = ld_stream(reinterpret_cast<const floatx4*>(g) + i0, NT);
+    mm[0] = ld_stream(reinterpret_cast<const floatx4*>(m) + i0, NT);
+    vv[0] = ld_stream(reinterpret_cast<const floatx4*>(v) + i0, NT);
     if (two) {
-      pp[1] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(p) + i1);
-      gg[1] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(g) + i1);
-      mm[1] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(m) + i1);
-      vv[1] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(v) + i1);
+      pp[1] = ld_stream(reinterpret_cast<const floatx4*>(p) + i1, NT);
+      gg[1] = ld_stream(reinterpret_cast<const floatx4*>(g) + i1, NT);
+      mm[1] = ld_stream(reinterpret_cast<const floatx4*>(m) + i1, NT);
+      vv[1] = ld_stream(reinterpret_cast<const floatx4*>(v) + i1, NT);
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -186,9 +195,9 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(
         const float denom = sqrtf(va[j]) * inv_sqrt_bc2 + eps;
         pa[j] = pa[j] * decay - step_size * ma[j] / denom;
       }
-      __builtin_nontemporal_store(pa, reinterpret_cast<floatx4*>(p) + i);
-      __builtin_nontemporal_store(ma, reinterpret_cast<floatx4*>(m) + i);
-      __builtin_nontemporal_store(va, reinterpret_cast<floatx4*>(v) + i);
+      st_stream(pa, reinterpret_cast<floatx4*>(p) + i, NT);
+      st_stream(ma, reinterpret_cast<floatx4*>(m) + i, NT);
+      st_stream(va, reinterpret_cast<floatx4*>(v) + i, NT);
       if (p16) {
         ushort4 o;
         o.x = Elt<T>::from_f(pa[0]);
@@ -349,6 +358,12 @@ extern "C" void fx_sumsq_f32(const float* x, long n, float* partial, int blocks,
   sumsq_f32_kernel<<<blocks, 256, 0, st>>>(x, n, partial);
 }
 
+static int g_adamw_grid = 0, g_adamw_nt = 1;  // tuning knobs (tools/bench_optim.py)
+extern "C" void fx_adamw_tune(int grid, int nt) {
+  g_adamw_grid = grid;
+  g_adamw_nt = nt;
+}
+
 extern "C" void fx_adamw_flat(int dtype, float* p, const float* g, float* m, float* v, void* p16,
                               long n, float lr, float beta1, float beta2, float eps, float wd,
                               float l2, const float* gscale, const int* skip, const int* step,
@@ -357,9 +372,16 @@ extern "C" void fx_adamw_flat(int dtype, float* p, const float* g, float* m, flo
   long blocks = (n / 4 + 511) / 512;
   const long cap = 256L * 8 * 4;
   int grid = (int)(blocks < 1 ? 1 : (blocks > cap ? cap : blocks));
-  FX_DISPATCH_T(dtype, adamw_flat_kernel<T><<<grid, 256, 0, st>>>(
-                           p, g, m, v, (uint16_t*)p16, n, lr, beta1, beta2, eps, wd, l2,
-                           gscale, skip, step));
+  if (g_adamw_grid > 0 && g_adamw_grid < grid) grid = g_adamw_grid;
+  if (g_adamw_nt) {
+    FX_DISPATCH_T(dtype, adamw_flat_kernel<T, true><<<grid, 256, 0, st>>>(
+                             p, g, m, v, (uint16_t*)p16, n, lr, beta1, beta2, eps, wd, l2,
+                             gscale, skip, step));
+  } else {
+    FX_DISPATCH_T(dtype, adamw_flat_kernel<T, false><<<grid, 256, 0, st>>>(
+                             p, g, m, v, (uint16_t*)p16, n, lr, beta1, beta2, eps, wd, l2,
+                             gscale, skip, step));
+  }
 }
 
 extern "C" void fx_cast_f32(int dtype, const float* x, void* y, long n, hipStream_t st) {

@@ -7,8 +7,12 @@ is HBM bound, so the figure of merit is TB/s against the ~8 TB/s peak.
 """
 import argparse
 import json
+import os
+import sys
 
-import torch
+sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), "..")))
+
+import torch  # noqa: E402
 
 
 def main():

@@ -17,6 +17,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=float, default=1e9)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--sweep", action="store_true", help="grid / non-temporal variants")
     a = ap.parse_args()
     from fleetx_amd.ops import _lib
     k = _lib.kernels()
@@ -35,19 +36,35 @@ def main():
         k.adamw_flat(0, p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p16.data_ptr(), n,
                      1e-4, 0.9, 0.95, 1e-8, 0.01, 0.0, gs.data_ptr(), skip.data_ptr(),
                      step.data_ptr(), _lib.stream())
-    for _ in range(2):
-        run()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(a.iters):
-        run()
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / a.iters
-    print(json.dumps({"kernel": "adamw_flat", "n": n, "ms": round(ms, 3),
-                      "TB_s": round(30.0 * n / ms / 1e9, 3),
-                      "ms_per_6.65B_params": round(ms * 6.65e9 / n, 2)}))
+    def timeit(fn):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / a.iters
+
+    # streaming references: copy (1 read + 1 write) and a*b -> c (2 reads + 1 write)
+    ms = timeit(lambda: m.copy_(p))
+    print(json.dumps({"kernel": "torch_copy_f32", "n": n, "ms": round(ms, 3),
+                      "TB_s": round(8.0 * n / ms / 1e9, 3)}))
+    ms = timeit(lambda: torch.mul(p, g, out=v))
+    print(json.dumps({"kernel": "torch_mul_f32", "n": n, "ms": round(ms, 3),
+                      "TB_s": round(12.0 * n / ms / 1e9, 3)}))
+    m.zero_()
+    v.zero_()
+    for grid, nt in ((0, 1), (0, 0), (1024, 1), (2048, 1), (4096, 1), (2048, 0)):
+        if a.sweep or (grid, nt) == (0, 1):
+            k.adamw_tune(grid, nt)
+            ms = timeit(run)
+            print(json.dumps({"kernel": "adamw_flat", "grid": grid or "auto", "nontemporal": nt,
+                              "n": n, "ms": round(ms, 3), "TB_s": round(30.0 * n / ms / 1e9, 3),
+                              "ms_per_6.65B_params": round(ms * 6.65e9 / n, 2)}))
+    k.adamw_tune(0, 1)
 
 
 if __name__ == "__main__":
