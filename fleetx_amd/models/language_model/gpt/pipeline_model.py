@@ -125,7 +125,8 @@ class GPTForPretrainingPipe(nn.Module):
                 if last_v:
                     losses.append(y)
                 else:
-                    p2p.exchange(send_next=y)
+                    p2p.post(send_next=y)
+        p2p.drain()
         if self.is_last:
             return torch.stack(losses).sum()
         return None

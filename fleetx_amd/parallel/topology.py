@@ -110,6 +110,11 @@ class HybridCommunicateGroup:
         self._groups["check"] = self._build(self._check_groups())
         # first/last pipeline stage pairs for the tied embedding
         self._groups["embedding"] = self._build(self._embedding_groups())
+        # second communicator over each pipe group: backward-direction p2p
+        # (gradients flowing stage s+1 -> s) gets its own RCCL stream, so it
+        # never queues behind forward activations (parallel/pipeline.py)
+        self._groups["pipe_bwd"] = self._build(self.topo.axis_groups("pipe")) \
+            if pp > 1 else self._groups["pipe"]
 
     def _build(self, rank_lists):
         mine = None
@@ -163,6 +168,9 @@ class HybridCommunicateGroup:
 
     def get_pipe_parallel_group(self):
         return self._groups["pipe"]
+
+    def get_pipe_bwd_group(self):
+        return self._groups["pipe_bwd"]
 
     def get_sharding_parallel_group(self):
         return self._groups["sharding"]

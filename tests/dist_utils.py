@@ -21,6 +21,10 @@ def _worker(rank, world, port, fn, args, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), FLEETX_LOG_RANK0_ONLY="1")
     torch.set_num_threads(1)
+    hang = int(os.environ.get("FLEETX_TEST_HANG_DUMP", "0"))
+    if hang > 0:  # debugging aid: dump every thread's stack if the rank hangs
+        import faulthandler
+        faulthandler.dump_traceback_later(hang, exit=True)
     try:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         res = fn(rank, world, *args)

@@ -54,6 +54,7 @@ def main():
         res = {"gemm": name, "M": M, "N": N, "K": K}
         cases = {
             "fwd_x_wT": lambda: torch.nn.functional.linear(x, w),
+            "fwd_x_wT_bias": lambda: torch.nn.functional.linear(x, w, bias),
             "fwd_x_wt": lambda: torch.mm(x, wt),
             "dgrad_dy_w": lambda: torch.mm(dy, w),
             "dgrad_dy_wtT": lambda: torch.mm(dy, wt.t()),
