@@ -21,7 +21,8 @@
 //    ds_write pass); tile i+1 is in flight into the second LDS buffer while
 //    tile i computes, one vmcnt drain + barrier per tile.
 //  * blockIdx is remapped so the q-blocks of one (batch, head) run on one XCD
-//    (shared K/V stay in that XCD's L2); causal heavy blocks go first.
+//    (shared K/V stay in that XCD's L2); causal grids are issued heaviest
+//    block first across the XCD's heads (lpt_order).
 #include <type_traits>
 
 #include "fx_common.h"
@@ -205,6 +206,24 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
 }
 
+// Causal work order (longest-processing-time first).  A causal block's cost
+// grows with its distance from the diagonal, so dispatching (head, block) in
+// head-major order leaves the heaviest blocks of the LAST heads to start near
+// the end of the grid: the kernel's tail is one heavy block running alone.
+// Here the grid is cut into chunks of G = B*H/8 heads (one XCD's contiguous
+// share after xcd_remap, so a head's blocks still share that XCD's L2), and
+// inside a chunk every head's heaviest block is issued first, then every
+// head's second heaviest, and so on.  `rank` 0 = heaviest.  Bijective on
+// [0, nblk) for any B*H.
+__device__ __forceinline__ void lpt_order(int lid, int nper, int BH, int& bh, int& rank) {
+  const int G = BH >= 8 ? BH >> 3 : 1;
+  const int c = lid / (G * nper);
+  const int j = lid - c * G * nper;
+  const int Gc = min(G, BH - c * G);
+  rank = j / Gc;
+  bh = c * G + j % Gc;
+}
+
 // ============================================================================
 // forward: WG = 4 waves x 32 queries = 128 queries; KV tile = 64 keys
 // ============================================================================
@@ -216,8 +235,15 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
   const int nq = (P.Sq + 127) / 128;
   const int nblk = nq * P.B * P.H;
   const int lid = xcd_remap(blockIdx.x, nblk);
-  const int bh = lid / nq;
-  const int qblock = CAUSAL ? (nq - 1 - lid % nq) : (lid % nq);
+  int bh, qblock;
+  if constexpr (CAUSAL) {
+    int rank;
+    lpt_order(lid, nq, P.B * P.H, bh, rank);
+    qblock = nq - 1 - rank;
+  } else {
+    bh = lid / nq;
+    qblock = lid % nq;
+  }
   const int b = bh / P.H, hd = bh % P.H;
 
   const uint16_t* qp = P.q + b * P.sq_b + hd * P.sq_h;
@@ -405,8 +431,15 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
   const int nq = (P.Sq + 127) / 128;
   const int nblk = nq * P.B * P.H;
   const int lid = xcd_remap(blockIdx.x, nblk);
-  const int bh = lid / nq;
-  const int qblock = CAUSAL ? (nq - 1 - lid % nq) : (lid % nq);
+  int bh, qblock;
+  if constexpr (CAUSAL) {
+    int rank;
+    lpt_order(lid, nq, P.B * P.H, bh, rank);
+    qblock = nq - 1 - rank;
+  } else {
+    bh = lid / nq;
+    qblock = lid % nq;
+  }
   const int b = bh / P.H, hd = bh % P.H;
   const uint16_t* qp = P.q + b * P.sq_b + hd * P.sq_h;
   const uint16_t* kp = P.k + b * P.sk_b + hd * P.sk_h;
@@ -559,8 +592,13 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
   const int nk = (P.Sk + 127) / 128;
   const int nblk = nk * P.B * P.H;
   const int lid = xcd_remap(blockIdx.x, nblk);
-  const int bh = lid / nk;
-  const int kblock = lid % nk;  // causal: low key blocks are the heavy ones
+  int bh, kblock;  // causal: low key blocks are the heavy ones
+  if constexpr (CAUSAL) {
+    lpt_order(lid, nk, P.B * P.H, bh, kblock);
+  } else {
+    bh = lid / nk;
+    kblock = lid % nk;
+  }
   const int b = bh / P.H, hd = bh % P.H;
   const uint16_t* qp = P.q + b * P.sq_b + hd * P.sq_h;
   const uint16_t* kp = P.k + b * P.sk_b + hd * P.sk_h;

@@ -24,11 +24,13 @@ def main():
     ap.add_argument("--h", type=int, default=32)
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
     args = ap.parse_args()
     from fleetx_amd import ops
     B, S, H, D = args.b, args.s, args.h, args.d
-    qkv = torch.randn(B, S, H, 3, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
-    g = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float16
+    qkv = torch.randn(B, S, H, 3, D, device="cuda", dtype=dt, requires_grad=True)
+    g = torch.randn(B, S, H, D, device="cuda", dtype=dt)
     for causal in (True, False):
         for p in (0.0, 0.1):
             def fwd():
@@ -50,7 +52,8 @@ def main():
             tf /= args.iters
             tb /= args.iters
             flops = 4.0 * B * H * S * S * D * (0.5 if causal else 1.0)
-            print(json.dumps({"B": B, "S": S, "H": H, "D": D, "causal": causal, "dropout": p,
+            print(json.dumps({"B": B, "S": S, "H": H, "D": D, "dtype": args.dtype,
+                              "causal": causal, "dropout": p,
                               "fwd_ms": round(tf, 4), "bwd_ms": round(tb, 4),
                               "fwd_tflops": round(flops / tf / 1e9, 1),
                               "bwd_tflops": round(2.5 * flops / tb / 1e9, 1)}), flush=True)
