@@ -160,16 +160,23 @@ class EagerEngine(BasicEngine):
         if mode == "train":
             comm = configs.Distributed.get("comm", {}) or {}
             sh_grp = self.hcg.get_sharding_parallel_group() if self._sharding_stage >= 1 else None
-            if self._sharding_stage == 3:
-                # reference: group_sharded_parallel(level='p_g_os') (eager_engine.py:228-242)
+            red = {"float32": torch.float32, "bfloat16": torch.bfloat16,
+                   "float16": torch.float16}[str(comm.get("reduce_dtype", "float32"))]
+            if self._sharding_stage == 3 or (self._sharding_stage == 2 and self.hcg.pp_degree == 1):
+                # reference: group_sharded_parallel(level='p_g_os' / 'os_g')
+                # (eager_engine.py:228-242); stage 2 keeps whole parameters
+                # but only the owned fp32 gradient shard
                 from ...parallel.sharding import Stage3ParamGradBuffer
                 assert self.hcg.pp_degree == 1, \
                     "sharding stage 3 does not compose with pipeline parallelism"
                 self.buffer = Stage3ParamGradBuffer(
                     model, shard_group=sh_grp, dp_group=self.hcg.get_data_parallel_group(),
                     mp_group=self.hcg.get_model_parallel_group(),
-                    prefetch=comm.get("stage3_prefetch", True))
+                    prefetch=comm.get("stage3_prefetch", True), stage=self._sharding_stage,
+                    reduce_dtype=red)
             else:
+                # stage 1 (and stage 2 under pipeline parallelism, where the
+                # tied-embedding reduction needs the flat layout)
                 self.buffer = FlatParamGradBuffer(
                     model.named_parameters(), dp_group=self.hcg.get_data_parallel_group(),
                     shard_group=sh_grp if sh_grp is not None
@@ -178,7 +185,7 @@ class EagerEngine(BasicEngine):
                     embed_group=self.hcg.get_embedding_group() if self.hcg.pp_degree > 1 else None,
                     bucket_mb=comm.get("dp_bucket_mb", 256),
                     overlap=comm.get("overlap_grad_reduce", True),
-                    shard_stage=self._sharding_stage)
+                    shard_stage=self._sharding_stage, reduce_dtype=red)
             if self.lr_scheduler is None and "lr" in configs.Optimizer:
                 self.lr_scheduler = build_lr_scheduler(configs.Optimizer.lr)
             self.optimizer = build_optimizer(configs.Optimizer, self.buffer, self.lr_scheduler,

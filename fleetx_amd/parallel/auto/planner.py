@@ -107,13 +107,16 @@ def estimate(h, L, heads, V, s, global_batch, dp, mp, pp, sharding, stage, micro
     if stage >= 3 and pp > 1:
         return None  # ZeRO-3 does not compose with pipeline stages here
     # ---- memory
-    grads = 4.0 * p_local / (sharding if stage >= 2 else 1)
+    layer = (12.0 * h * h) / mp
+    grads = 4.0 * p_local
+    if stage >= 2 and pp == 1:
+        # owned fp32 shard + two layers of full fp32 grads in flight
+        # (parallel/sharding.py); under pp > 1 stage 2 keeps the flat layout
+        grads = 4.0 * p_local / sharding + 2 * 4.0 * layer
     opt = 12.0 * p_local / (sharding if stage >= 1 else 1)
     params = 2.0 * p_local
-    if stage >= 3:  # shards + two layers of full params / fp32 grads in flight
-        layer = (12.0 * h * h) / mp
+    if stage >= 3:  # shards + two layers of full params in flight
         params = 2.0 * p_local / sharding + 2 * 2.0 * layer
-        grads += 2 * 4.0 * layer
     layers_local = L // pp
     act_layer = (2.0 if recompute else 34.0 / mp) * s * micro * h
     in_flight = min(m, pp) if pp > 1 else 1  # 1F1B keeps <= pp micro-batches alive
@@ -145,6 +148,8 @@ def estimate(h, L, heads, V, s, global_batch, dp, mp, pp, sharding, stage, micro
         # every layer twice (forward + backward) under the layer compute
         rs = _rs_or_ag_s(gbytes, sharding)
         ag = _rs_or_ag_s(2.0 * p_local, sharding)
+        if stage >= 2 and pp == 1:
+            rs *= m  # stage 2/3 reduce-scatter every micro-batch's gradient
         grad = _rs_or_ag_s(bucket, sharding) + max(0.0, rs - comp * 0.6)
         grad += max(0.0, ag - comp * 0.3) if stage < 3 else max(0.0, 2 * ag - comp * 0.8)
     else:

@@ -9,6 +9,10 @@ Capability parity:
 * P06 sharding stage 1/2 gradient path (reduce-scatter to the owning rank);
 * N09 coalesced mp all-reduce of sequence-parallel replicated grads;
 * N11 tied-embedding grad all-reduce between first and last pipeline stage.
+* ``reduce_dtype`` (``Distributed.comm.reduce_dtype``: float32 default,
+  bfloat16 / float16 like the reference's fp16 gradient all-reduce) puts a
+  16-bit copy of each bucket on the wire -- half the xGMI bytes -- and the
+  result lands back in the fp32 gradient.
 
 MI355X design:
 * every trainable parameter becomes a VIEW into one model-dtype flat buffer
@@ -285,6 +289,8 @@ class FlatParamGradBuffer:
         works = []
         if self._norm_stream is not None:  # _launch only runs on final gradients
             self._early_norm_bucket(b)
+        low = self.reduce_dtype != torch.float32
+        src = seg.to(self.reduce_dtype) if low else seg   # 16-bit wire copy
         if self.shard_stage >= 1 and self.shard_group is not None:
             # reduce-scatter to the owner (in place: RCCL's recvbuff = sendbuff + rank*count);
             # dp all-reduce of the owned shard follows in finish()
@@ -293,16 +299,22 @@ class FlatParamGradBuffer:
             chunk = (b.end - b.start) // n
             out = self.grad_flat[b.start + r * chunk:b.start + (r + 1) * chunk]
             if _is_gloo(self.shard_group):
-                works.append(dist.all_reduce(seg, group=self.shard_group.group, async_op=True))
+                works.append(dist.all_reduce(src, group=self.shard_group.group, async_op=True))
+                wire = src[r * chunk:(r + 1) * chunk] if low else None
+            elif low:
+                wire = torch.empty(chunk, dtype=self.reduce_dtype, device=seg.device)
+                works.append(dist.reduce_scatter_tensor(wire, src, group=self.shard_group.group,
+                                                        async_op=True))
             else:
+                wire = None
                 works.append(dist.reduce_scatter_tensor(out, seg, group=self.shard_group.group,
                                                         async_op=True))
-            b.work = ("rs", works, out)
+            b.work = ("rs", works, out, wire)
         else:
             grp = self.dp_group
             if grp is not None:
-                works.append(dist.all_reduce(seg, group=grp.group, async_op=True))
-            b.work = ("ar", works, seg)
+                works.append(dist.all_reduce(src, group=grp.group, async_op=True))
+            b.work = ("ar", works, seg, src if (low and grp is not None) else None)
 
     def finish(self):
         """Complete every gradient collective; average over the data world."""
@@ -319,9 +331,11 @@ class FlatParamGradBuffer:
         if self.shard_group is not None:
             data_world *= self.shard_group.nranks
         for b in self.buckets:
-            kind, works, seg = b.work
+            kind, works, seg, wire = b.work
             for w in works:
                 w.wait()
+            if wire is not None:  # 16-bit reduction: back into the fp32 gradient
+                seg.copy_(wire)
             if kind == "rs" and self.dp_group is not None:
                 dist.all_reduce(seg, group=self.dp_group.group)
             if data_world > 1:

@@ -1,5 +1,6 @@
-"""ZeRO stage 3: parameters, gradients and optimizer state all partitioned
-over the sharding group, with layer-granular gather / release.
+"""ZeRO stage 3 (parameters, gradients and optimizer state partitioned over
+the sharding group, layer-granular gather / release) and ZeRO stage 2
+(gradients and optimizer state partitioned, parameters kept whole).
 
 Capability parity: reference ``group_sharded_parallel(level='p_g_os')``
 reached from ``eager_engine.py:221-242`` (P06) and the save-time
@@ -34,6 +35,17 @@ MI355X design (not a translation of Paddle's GroupShardedStage3):
   following layer's backward.
 * Peak per-rank memory: (params + grads + Adam state) / nshard plus two
   layers of full parameters and fp32 grads in flight.
+* **Stage 2** (reference ``level='os_g'``, ``eager_engine.py:228-242``) is the
+  same gradient path with the parameters never released: every rank keeps the
+  whole model-dtype parameters, but a unit's fp32 gradient buffer exists only
+  from its first gradient to the completion of its reduce-scatter, and only
+  the owned fp32 shard survives the step (grads / nshard resident instead of
+  the whole fp32 gradient).  After the sharded update the parameters are
+  re-assembled by asynchronous all-gathers that each unit's forward pre-hook
+  waits for, so the gather hides under the next forward.
+* ``reduce_dtype`` = bfloat16 / float16 (``Distributed.comm.reduce_dtype``)
+  reduce-scatters a 16-bit copy of the gradient (half the xGMI bytes) and
+  accumulates the owned piece in fp32.
 """
 import contextlib
 
@@ -113,10 +125,15 @@ class Stage3ParamGradBuffer:
     """
 
     def __init__(self, model, shard_group, dp_group=None, mp_group=None,
-                 decay_fn=default_decay_fn, prefetch=True, fused_wgrad=True):
-        assert shard_group is not None and shard_group.nranks > 1, "stage 3 needs sharding > 1"
+                 decay_fn=default_decay_fn, prefetch=True, fused_wgrad=True, stage=3,
+                 reduce_dtype=torch.float32):
+        assert shard_group is not None and shard_group.nranks > 1, \
+            "stage %d needs sharding > 1" % stage
+        assert stage in (2, 3)
         self.shard_group = shard_group
-        self.shard_stage = 3
+        self.shard_stage = stage
+        self.shard_params = stage >= 3
+        self.reduce_dtype = reduce_dtype
         self.dp_group = dp_group if dp_group is not None and dp_group.nranks > 1 else None
         self.mp_group = mp_group if mp_group is not None and mp_group.nranks > 1 else None
         self.embed_group = None
@@ -208,7 +225,8 @@ class Stage3ParamGradBuffer:
             u.gathered = True
             u.grad_live = True
             self._writeback_shard(u)
-            self._release_params(u)
+            if self.shard_params:
+                self._release_params(u)
             self._release_grads(u)
         self._install_hooks(model)
 
@@ -251,6 +269,8 @@ class Stage3ParamGradBuffer:
         if not u.gathered:
             return
         self._wait_gather(u)
+        if not self.shard_params:  # stage 2: parameters stay whole
+            return
         _free(u.full_param)
         u.gathered = False
 
@@ -367,12 +387,14 @@ class Stage3ParamGradBuffer:
         works, pieces = [], []
         for seg in u.segments:
             full = u.full_grad[seg.fstart:seg.fend]
+            if self.reduce_dtype != torch.float32:
+                full = full.to(self.reduce_dtype)
             piece = self._piece(seg)
             if self.gloo:
                 dist.all_reduce(full, group=self.shard_group.group)
                 red = full[self.rank * piece:(self.rank + 1) * piece]
             else:
-                red = torch.empty(piece, dtype=torch.float32, device=self.device)
+                red = torch.empty(piece, dtype=full.dtype, device=self.device)
                 works.append(dist.reduce_scatter_tensor(red, full, group=self.shard_group.group,
                                                         async_op=True))
             pieces.append((seg, red))
@@ -449,7 +471,30 @@ class Stage3ParamGradBuffer:
         return [(c.start, c.end, c) for c in self.category_list]
 
     def allgather_params(self):
-        """No-op: parameters are gathered lazily by the next forward."""
+        """Stage 3: no-op (parameters are gathered lazily by the next forward).
+        Stage 2: re-assemble every unit from the updated shards, asynchronously
+        in forward order; each unit's forward pre-hook waits for its own."""
+        if self.shard_params:
+            return
+        for u in self.all_units:
+            self._wait_gather(u)
+            works = []
+            for seg in u.segments:
+                out = u.full_param[seg.fstart:seg.fend]
+                mine = self.param_flat[seg.sstart:seg.send]
+                if self.gloo:
+                    parts = [torch.empty_like(mine) for _ in range(self.nsh)]
+                    dist.all_gather(parts, mine, group=self.shard_group.group)
+                    out.copy_(torch.cat(parts))
+                else:
+                    works.append(dist.all_gather_into_tensor(out, mine,
+                                                             group=self.shard_group.group,
+                                                             async_op=True))
+            u.gather_works = works
+
+    def sync_params(self):
+        for u in self.all_units:
+            self._wait_gather(u)
 
     @contextlib.contextmanager
     def gathered(self, writeback=False):
@@ -471,7 +516,10 @@ class Stage3ParamGradBuffer:
         """Bytes resident per rank (shards) vs. what an unsharded layout holds."""
         full = sum(u.numel for u in self.all_units)
         esz = self.param_flat.element_size()
-        return {"shard_param_bytes": self.param_flat.numel() * esz,
+        return {"stage": self.shard_stage,
+                "resident_param_bytes": (self.param_flat.numel() if self.shard_params
+                                         else full) * esz,
+                "shard_param_bytes": self.param_flat.numel() * esz,
                 "shard_grad_bytes": self.grad_flat.numel() * 4,
                 "unsharded_param_bytes": full * esz,
                 "unsharded_grad_bytes": full * 4}

@@ -154,7 +154,21 @@ def test_sharding_stage3_with_tp(ref_losses):
     _check(dist_utils.run(_train, 4, (1, 2, 1, 2, 3, 4, False, 1)), ref_losses)
 
 
-def _stage3_memory_and_resume(rank, world, outdir):
+def test_sharding_stage2_dp_and_accumulation(ref_losses):
+    # ZeRO-2 (owned fp32 grad shards, whole params), 2 accumulation steps
+    _check(dist_utils.run(_train, 4, (2, 1, 1, 2, 2, 1, False, 1)), ref_losses)
+
+
+@pytest.mark.parametrize("layout", [(2, 1, 1, 1, 0, 4, False, 1), (1, 1, 1, 2, 1, 4, False, 1),
+                                    (1, 1, 1, 2, 2, 4, False, 1)])
+def test_reduce_dtype_bf16(ref_losses, layout):
+    """Distributed.comm.reduce_dtype=bfloat16: 16-bit gradient reductions
+    (reference fp16 all-reduce) stay within bf16 rounding of the fp32 curve."""
+    out = dist_utils.run(_train, 2, layout, 3, ("Distributed.comm.reduce_dtype=bfloat16",))
+    _check(out, ref_losses, tol=5e-3)
+
+
+def _stage3_memory_and_resume(rank, world, outdir, stage=3):
     """Shards are 1/n of the model; save gathers full params; a fresh
     engine that loads the checkpoint continues the identical loss curve."""
     from fleetx_amd.utils import config as C
@@ -170,7 +184,7 @@ def _stage3_memory_and_resume(rank, world, outdir):
               "Model.attention_probs_dropout_prob=0.0", "Model.max_position_embeddings=64",
               "Global.device=cpu", "Global.local_batch_size=4", "Global.micro_batch_size=4",
               "Distributed.dp_degree=1", "Distributed.sharding.sharding_degree=2",
-              "Distributed.sharding.sharding_stage=3", "Engine.max_steps=10",
+              "Distributed.sharding.sharding_stage=%d" % stage, "Engine.max_steps=10",
               "Engine.save_load.output_dir=%s" % outdir,
               "Data.Train.dataset.name=SyntheticGPTDataset"] + list(extra)
         cfg = C.get_config(CFG, overrides=ov, nranks=world)
@@ -199,11 +213,18 @@ def _stage3_memory_and_resume(rank, world, outdir):
     return {"rep": rep, "cont": cont, "res": res}
 
 
-def test_sharding_stage3_memory_and_resume(tmp_path):
-    out = dist_utils.run(_stage3_memory_and_resume, 2, str(tmp_path))
+@pytest.mark.parametrize("stage", [2, 3])
+def test_sharding_memory_and_resume(tmp_path, stage):
+    out = dist_utils.run(_stage3_memory_and_resume, 2, str(tmp_path), stage)
     for r in out:
         rep = r["rep"]
-        assert rep["shard_param_bytes"] * 2 == rep["unsharded_param_bytes"]
+        assert rep["stage"] == stage
+        # ZeRO-2 and 3 keep only the owned fp32 gradient shard
+        assert rep["shard_grad_bytes"] * 2 == rep["unsharded_grad_bytes"]
+        if stage == 3:
+            assert rep["resident_param_bytes"] * 2 == rep["unsharded_param_bytes"]
+        else:
+            assert rep["resident_param_bytes"] == rep["unsharded_param_bytes"]
         for a, b in zip(r["cont"], r["res"]):
             assert abs(a - b) < 1e-6, (r["cont"], r["res"])
     assert (tmp_path / "epoch_0_step_2" / "mp_00_sharding_01_pp_00" / "model.pdparams").exists()
