@@ -157,8 +157,13 @@ class EagerEngine(BasicEngine):
 
         self.buffer, self.optimizer, self.lr_scheduler = None, optimizer, lr
         self.scaler = None
+        comm = configs.Distributed.get("comm", {}) or {}
+        # TP / SP communication-compute overlap (parallel/linear.py, sp_overlap.py)
+        from ...parallel import layers as _layers, sp_overlap as _spo
+        _layers.TP_OVERLAP["enabled"] = bool(comm.get("tp_overlap", True))
+        _layers.TP_OVERLAP["row_chunks"] = int(comm.get("tp_row_chunks", 2))
+        _spo.SP_CHUNKS["chunks"] = int(comm.get("sp_chunks", 2))
         if mode == "train":
-            comm = configs.Distributed.get("comm", {}) or {}
             sh_grp = self.hcg.get_sharding_parallel_group() if self._sharding_stage >= 1 else None
             red = {"float32": torch.float32, "bfloat16": torch.bfloat16,
                    "float16": torch.float16}[str(comm.get("reduce_dtype", "float32"))]

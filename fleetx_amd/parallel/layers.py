@@ -29,6 +29,7 @@ from . import mappings as M
 from . import topology as topo
 from .. import ops
 from .linear import linear, column_tp_linear, row_tp_linear
+from .sp_overlap import column_sp_linear, row_sp_linear
 
 
 # Tensor-parallel comm/compute overlap switches (Distributed.comm.tp_overlap*)
@@ -109,8 +110,11 @@ class ColumnParallelLinear(nn.Module):
     def forward(self, x):
         b = None if self.skip_bias_add else self.bias
         if self.sequence_parallel:
-            x = M.all_gather_seq(x)
-            y = linear(x, self.weight, b)
+            if TP_OVERLAP["enabled"] and x.dim() == 3:
+                y = column_sp_linear(x, self.weight, b, topo.mp_group())
+            else:
+                x = M.all_gather_seq(x)
+                y = linear(x, self.weight, b)
         elif topo.mp_world_size() > 1 and TP_OVERLAP["enabled"]:
             y = column_tp_linear(x, self.weight, b, topo.mp_group())
         else:
@@ -153,7 +157,10 @@ class RowParallelLinear(nn.Module):
         if not self.input_is_parallel:
             x = M.scatter_to_mp(x)
         if self.sequence_parallel:
-            y = M.reduce_scatter_seq(linear(x, self.weight))
+            if TP_OVERLAP["enabled"] and x.dim() == 3 and x.shape[0] % topo.mp_world_size() == 0:
+                y = row_sp_linear(x, self.weight, topo.mp_group())
+            else:
+                y = M.reduce_scatter_seq(linear(x, self.weight))
         elif topo.mp_world_size() > 1 and TP_OVERLAP["enabled"]:
             y = row_tp_linear(x, self.weight, topo.mp_group(), TP_OVERLAP["row_chunks"])
         else:

@@ -79,8 +79,9 @@ def _tn_operands(dy2, x2, colsum=None):
     return transpose2d(dy2, colsum=colsum), transpose2d(x2).t()
 
 
-def accumulate_wgrad(weight, dy2, x2, bias=None):
-    """``weight.main_grad (+)= dy2^T @ x2`` in fp32; notifies the grad buffer.
+def accumulate_wgrad(weight, dy2, x2, bias=None, notify=True):
+    """``weight.main_grad (+)= dy2^T @ x2`` in fp32; notifies the grad buffer
+    (``notify=False``: a partial contribution, more follow in this backward).
 
     With ``bias`` (a Parameter) the bias gradient ``sum_rows(dy2)`` is produced
     too: straight into ``bias.main_grad`` when the bias takes fused grads
@@ -99,7 +100,8 @@ def accumulate_wgrad(weight, dy2, x2, bias=None):
                 colsum_into(dy2, db, False)
                 db = db.to(bias.dtype)
         weight._fx_fresh = False
-        grad_part_done(weight)
+        if notify:
+            grad_part_done(weight)
         return db
     db, colsum = None, None
     if bias is not None:
@@ -139,7 +141,8 @@ def accumulate_wgrad(weight, dy2, x2, bias=None):
         else:
             mg.add_(g)
     weight._fx_fresh = False
-    grad_part_done(weight)
+    if notify:
+        grad_part_done(weight)
     return db
 
 

@@ -189,6 +189,9 @@ def _fill_defaults(config):
     comm.setdefault("dp_bucket_mb", 256)        # few, large RCCL calls over xGMI
     comm.setdefault("overlap_grad_reduce", True)
     comm.setdefault("reduce_dtype", "float32")
+    comm.setdefault("tp_overlap", True)         # async dX all-reduce / chunked row all-reduce
+    comm.setdefault("tp_row_chunks", 2)
+    comm.setdefault("sp_chunks", 2)             # SP all-gather / reduce-scatter chunks
     eng = config.setdefault("Engine", AttrDict())
     mp = eng.setdefault("mix_precision", AttrDict())
     mp.setdefault("use_pure_fp16", False)

@@ -110,6 +110,13 @@ def test_sequence_parallel(ref_losses):
     _check(dist_utils.run(_train, 2, (1, 2, 1, 1, 0, GBS, True, 1)), ref_losses)
 
 
+@pytest.mark.parametrize("extra", [("Distributed.comm.sp_chunks=4",),
+                                   ("Distributed.comm.tp_overlap=False",)])
+def test_sequence_parallel_overlap_variants(ref_losses, extra):
+    """Chunked overlapped SP linears (4 chunks) and the plain gather/scatter path."""
+    _check(dist_utils.run(_train, 2, (1, 2, 1, 1, 0, GBS, True, 1), 3, extra), ref_losses)
+
+
 def test_pipeline_1f1b(ref_losses):
     _check(dist_utils.run(_train, 2, (1, 1, 2, 1, 0, 2, False, 1)), ref_losses)
 
