@@ -1,0 +1,89 @@
+"""Pure-fp16 (O2) training on the GPU: the reference's ``use_pure_fp16: True,
+dtype: float16`` mode (``pretrain_gpt_base.yaml:18-22``,
+``eager_engine.py:157-167,421,436-438``) through the f16 MFMA flash kernels,
+fused LN / CE and the device-side dynamic loss scaler.
+
+* fp16 and bf16 runs from identical weights follow the same loss curve;
+* an injected overflow (loss scale 2^40 -> inf fp16 gradients) skips the
+  update entirely (parameters and Adam's step counter unchanged) and the
+  scale halves only after ``decr_every_n_nan_or_inf`` (2) consecutive
+  overflows (Paddle GradScaler semantics)."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CFG = os.path.join(os.path.dirname(__file__), "..", "fleetx_amd", "configs", "nlp", "gpt",
+                   "pretrain_gpt_345M_single_card.yaml")
+B, S, V = 4, 256, 2048
+
+
+def _engine(dtype):
+    from fleetx_amd.utils import config as C
+    from fleetx_amd.utils import env
+    from fleetx_amd.models import build_module
+    from fleetx_amd.core.engine.eager_engine import EagerEngine
+    from fleetx_amd.parallel import topology as topo
+    topo.reset_hcg()
+    ov = ["Model.hidden_size=512", "Model.num_layers=2", "Model.num_attention_heads=8",
+          "Model.vocab_size=%d" % V, "Model.hidden_dropout_prob=0.0",
+          "Model.attention_probs_dropout_prob=0.0", "Model.max_position_embeddings=%d" % S,
+          "Global.device=gpu", "Global.local_batch_size=%d" % B, "Global.micro_batch_size=%d" % B,
+          "Engine.mix_precision.use_pure_fp16=True", "Engine.mix_precision.dtype=%s" % dtype,
+          "Engine.mix_precision.scale_loss=1024.0", "Engine.max_steps=100",
+          "Data.Train.dataset.name=SyntheticGPTDataset"]
+    cfg = C.get_config(CFG, overrides=ov, nranks=1)
+    cfg.Optimizer.lr = {"name": "ConstantLR", "learning_rate": 1e-3}
+    env.init_dist_env(cfg)
+    env.set_seed(cfg.Global.seed)
+    return EagerEngine(configs=cfg, module=build_module(cfg), mode="train")
+
+
+def _batch(step):
+    g = torch.Generator().manual_seed(100 + step)
+    t = torch.randint(0, V, (B, S + 1), generator=g).cuda()
+    return [t[:, :-1].contiguous(), torch.arange(S, device="cuda").expand(B, S).contiguous(),
+            t[:, 1:].contiguous(), torch.ones(B, S, device="cuda")]
+
+
+def test_fp16_matches_bf16_curve():
+    curves = {}
+    for dt in ("bfloat16", "float16"):
+        eng = _engine(dt)
+        assert eng._dtype == getattr(torch, dt)
+        assert (eng.scaler is not None) == (dt == "float16")
+        # the same batch every step: the loss must fall
+        curves[dt] = [eng._reduce_log_loss(eng._fit_impl(_batch(0)), 1) for s in range(4)]
+    a, b = curves["float16"], curves["bfloat16"]
+    for x, y in zip(a, b):
+        assert abs(x - y) < 1e-2 * abs(y), curves
+    assert a[-1] < a[0], curves
+
+
+def test_fp16_overflow_skips_update_and_scaler_backs_off():
+    eng = _engine("float16")
+    eng._fit_impl(_batch(0))                     # one clean step
+    torch.cuda.synchronize()
+    opt, sc = eng.optimizer, eng.scaler
+    step0 = int(opt.dev_step.item())
+    params0 = eng.buffer.param_flat.clone()
+    sc.scale.fill_(2.0 ** 40)                    # fp16 gradients overflow
+    eng.optimizer.loss_scale = sc.scale
+    eng._fit_impl(_batch(1))
+    torch.cuda.synchronize()
+    assert int(opt.found_inf.item()) == 1
+    assert torch.equal(eng.buffer.param_flat, params0), "overflowed step changed the weights"
+    assert int(opt.dev_step.item()) == step0, "overflowed step advanced Adam's bias correction"
+    assert float(sc.scale) == 2.0 ** 40 and int(sc.bad) == 1   # 1st overflow: keep the scale
+    eng._fit_impl(_batch(2))
+    torch.cuda.synchronize()
+    assert float(sc.scale) == 2.0 ** 39 and int(sc.bad) == 0   # 2nd consecutive: halve
+    sc.scale.fill_(1024.0)
+    eng.optimizer.loss_scale = sc.scale
+    eng._fit_impl(_batch(3))
+    torch.cuda.synchronize()
+    assert int(opt.found_inf.item()) == 0
+    assert int(opt.dev_step.item()) == step0 + 1
+    assert not torch.equal(eng.buffer.param_flat, params0)
