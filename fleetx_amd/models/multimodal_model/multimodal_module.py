@@ -91,7 +91,13 @@ class ImagenModule(MultiModalModule):
         if name not in imagen.BUILDERS:
             raise ValueError("unknown imagen model {} (known: {})".format(name,
                                                                            sorted(imagen.BUILDERS)))
-        return imagen.BUILDERS[name](**dict(m))
+        model = imagen.BUILDERS[name](**dict(m))
+        q = self.configs.get("Quantization")
+        if q is not None and q.get("enable", False):
+            # reference multimodal_module.py:86-89 (QAT over Conv2D / Conv2DTranspose / Linear)
+            from ...utils.qat import quantize_model
+            model = quantize_model(model, q)
+        return model
 
     def get_loss_fn(self):
         return imagen.ImagenCriterion(**dict(copy.deepcopy(self.configs.get("Loss", {}) or {})))
