@@ -38,6 +38,13 @@ def _pairs(word):
 PAT = re.compile(r"""'s|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\p{N}+| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+""")
 
 
+
+# reference gpt_tokenizer.py pretrained resource URLs (vocab, merges)
+PRETRAINED_URLS = {
+    "gpt2": ("http://fleet.bj.bcebos.com/datasets/gpt/gpt2-vocab.json",
+             "http://fleet.bj.bcebos.com/datasets/gpt/gpt2-merges.txt"),
+}
+
 class GPTTokenizer:
     eos_token = "<|endoftext|>"
 
@@ -79,6 +86,16 @@ class GPTTokenizer:
                 m = os.path.join(d, "gpt2-merges.txt")
             if os.path.exists(v) and os.path.exists(m):
                 return cls(v, m, **kwargs)
+        # the reference's hosted vocab (gpt_tokenizer.py:126-128) through the
+        # offline cache: found if a previous run / the user put it there
+        urls = PRETRAINED_URLS.get(str(name_or_dir))
+        if urls is not None:
+            from ...utils.download import cached_path
+            try:
+                return cls(cached_path(urls[0], cache_dir), cached_path(urls[1], cache_dir),
+                           **kwargs)
+            except (FileNotFoundError, TimeoutError):
+                pass
         raise FileNotFoundError(
             "GPT-2 tokenizer files not found (looked in {}). Place vocab.json and merges.txt in "
             "one of these directories or set FLEETX_TOKENIZER_DIR; FleetX-AMD never downloads."

@@ -37,10 +37,27 @@ def init_dist_env(config, backend=None):
         os.environ.setdefault("TORCH_DISTRIBUTED_DEBUG", "DETAIL")
     elif dbg == "info":
         os.environ.setdefault("TORCH_DISTRIBUTED_DEBUG", "INFO")
+    _check_env(config)
     topo.init_distributed(backend=backend, timeout_s=int(d.get("timeout_s", 1800) or 1800))
     hcg = topo.init_hcg(dp=d.dp_degree, mp=d.mp_degree, pp=d.pp_degree,
                         sharding=d.sharding.sharding_degree)
     return hcg
+
+
+def _check_env(config):
+    """Reference ``config.py:242-245``: version check always, GPU check when
+    ``Global.device`` is gpu (a missing GPU is reported, then the run falls
+    back to CPU as ``env.device()`` does; a non-gfx950 GPU is reported)."""
+    from . import check
+    from .log import logger
+    check.version_check(exit=False)
+    if str((config.get("Global", {}) or {}).get("device", "gpu")).lower() in ("gpu", "cuda"):
+        try:
+            arch = check.check_gpu(require_gfx950=False, exit=False)
+            if not str(arch).startswith("gfx950"):
+                logger.warning("GPU %s is not gfx950 (MI355X): the HIP kernels will not load", arch)
+        except RuntimeError as e:
+            logger.warning("%s -- running on CPU", e)
 
 
 def get_data_world_size():
