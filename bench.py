@@ -33,7 +33,8 @@ MODELS = {
     "gpt-345M": (1024, 24, 16),
     "gpt-tiny": (256, 2, 4),
 }
-PEAK_BF16 = 2.5e15  # MI355X dense bf16 (spec), per GPU
+from fleetx_amd.utils.hw import PEAK_DENSE_FLOPS  # noqa: E402
+PEAK_BF16 = PEAK_DENSE_FLOPS["bfloat16"]  # MI355X dense bf16 (spec), per GPU
 # Reference (V100) throughput per GPU on the same model/batch/seq:
 # row 1 (345M single card, 16.2k tokens/s) and row 4 (1.3B dp8, ~3.3k tokens/s/GPU,
 # derived).  The 6.7B headline config has no published reference number.

@@ -52,9 +52,23 @@ class LanguageModule(BasicModule):
         tokens = self.configs.Global.global_batch_size * self._seq_len()
         logger.info(
             "[train] epoch: %d, batch: %d, loss: %.9f, avg_batch_cost: %.5f sec, speed: %.2f step/s, "
-            "ips_total: %.0f tokens/s, ips: %.0f tokens/s, learning rate: %.5e"
+            "ips_total: %.0f tokens/s, ips: %.0f tokens/s, learning rate: %.5e, mfu: %.1f%%"
             % (log_dict["epoch"], log_dict["batch"], log_dict["loss"], log_dict["train_cost"], speed,
-               speed * tokens, speed * tokens / self.data_world_size, log_dict["lr"]))
+               speed * tokens, speed * tokens / self.data_world_size, log_dict["lr"],
+               100.0 * self.mfu(speed * tokens)))
+
+    def mfu(self, tokens_per_s):
+        """Model FLOPs utilisation of the whole job: useful
+        training FLOPs (6N + attention, no recompute) / (GPUs x dense peak)."""
+        from ...utils import hw
+        from .gpt.model import flops_per_token
+        try:
+            fpt = flops_per_token(self.gpt_config, self._seq_len())
+        except Exception:
+            return 0.0
+        n = max(1, env.get_world_size())
+        dt = str(getattr(self.gpt_config, "dtype", "bfloat16") or "bfloat16")
+        return tokens_per_s * fpt / (n * hw.peak_flops(dt))
 
     def tokens_per_step(self):
         """Tokens of one optimizer step over the whole job (the ips_total numerator)."""

@@ -29,9 +29,10 @@ def init_dist_env(config, backend=None):
     """Create the process group and the hybrid topology from ``Distributed``."""
     set_debug_modes(config)
     d = config.Distributed
-    # collective debugging (SURVEY §5.2, new vs. the reference): "detail" wraps every
-    # process group so each collective first cross-checks op / shape / dtype
-    # fingerprints across ranks and reports the mismatching rank instead of hanging.
+    # collective debugging (SURVEY §5.2, new vs. the reference): "fingerprint"
+    # cross-checks every collective's op / sequence number / shape / dtype over
+    # gloo mirrors and names the diverging rank; "detail" / "info" additionally
+    # turn on torch's TORCH_DISTRIBUTED_DEBUG checks.
     dbg = str(d.get("debug", os.environ.get("FLEETX_COLLECTIVE_CHECK", "off")) or "off").lower()
     if dbg in ("1", "detail", "on", "true"):
         os.environ.setdefault("TORCH_DISTRIBUTED_DEBUG", "DETAIL")
@@ -41,6 +42,11 @@ def init_dist_env(config, backend=None):
     topo.init_distributed(backend=backend, timeout_s=int(d.get("timeout_s", 1800) or 1800))
     hcg = topo.init_hcg(dp=d.dp_degree, mp=d.mp_degree, pp=d.pp_degree,
                         sharding=d.sharding.sharding_degree)
+    if dbg == "fingerprint":
+        # per-collective op / sequence / shape / dtype cross-check over gloo
+        # mirrors of every group (parallel/collective_check.py)
+        from ..parallel import collective_check
+        collective_check.enable(hcg)
     return hcg
 
 

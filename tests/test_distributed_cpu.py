@@ -245,3 +245,11 @@ def test_sharding_rccl_collective_forms(ref_losses, monkeypatch, stage, dp, micr
     monkeypatch.setenv("FLEETX_GLOO_AS_RCCL", "1")
     world = 2 * dp
     _check(dist_utils.run(_train, world, (dp, 1, 1, 2, stage, micro, False, 1)), ref_losses)
+
+
+@pytest.mark.parametrize("layout", [(2, 1, 1, 1, 0, 4, False, 1), (1, 2, 1, 2, 2, 4, False, 1)])
+def test_fingerprint_mode_trains_identically(ref_losses, layout):
+    """Distributed.debug=fingerprint checks every collective of a real step."""
+    world = layout[0] * layout[1] * layout[2] * layout[3]
+    _check(dist_utils.run(_train, world, layout, 3, ("Distributed.debug=fingerprint",)),
+           ref_losses)
