@@ -409,7 +409,11 @@ class EagerEngine(BasicEngine):
                 torch.cuda.synchronize()
             cost = time.time() - t0
             if (i + 1) % self._logging_freq == 0:
-                lval = float(loss.float().item()) if torch.is_tensor(loss) else loss
+                if self._pipeline:
+                    # the loss lives on the last stage: broadcast it to every stage
+                    lval = self._reduce_log_loss(loss, 1)
+                else:
+                    lval = float(loss.float().item()) if torch.is_tensor(loss) else loss
                 self._module.validation_step_end({"epoch": epoch, "batch": i, "loss": lval,
                                                   "eval_cost": cost / self._logging_freq,
                                                   "total_batch": total})

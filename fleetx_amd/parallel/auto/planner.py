@@ -172,7 +172,7 @@ def plan(h, L, heads, V, s, global_batch, world, allow_recompute=True, prefer=No
 
 def _plan(h, L, heads, V, s, global_batch, world, allow_recompute, prefer, zero_stages):
     divs = [d for d in range(1, world + 1) if world % d == 0]
-    best = None
+    cands = []
     for mp, pp in itertools.product(divs, divs):
         if world % (mp * pp):
             continue
@@ -196,16 +196,19 @@ def _plan(h, L, heads, V, s, global_batch, world, allow_recompute, prefer, zero_
                     if r is None:
                         continue
                     t, mem = r
-                    # on (10 ms) ties prefer the lower ZeRO stage, no recompute, less memory
-                    key = (round(t, 2), stage, int(recompute), mem)
-                    if best is None or key < best[0]:
-                        best = (key, Plan(dp, mp, pp, sharding, stage if sharding > 1 else 0,
-                                          micro, recompute, False, t, mem / 1e9,
-                                          global_batch * s / t))
-    if best is None:
+                    cands.append((t, stage, int(recompute), -micro, mem,
+                                  Plan(dp, mp, pp, sharding, stage if sharding > 1 else 0,
+                                       micro, recompute, False, t, mem / 1e9,
+                                       global_batch * s / t)))
+    if not cands:
         raise ValueError("no feasible layout for world={} within {:.0f} GB".format(
             world, HBM_BYTES * USABLE / 1e9))
-    return best[1]
+    # layouts within 1 % of the fastest estimate are ties (the model is not
+    # that precise): prefer the lower ZeRO stage, no recompute, the larger
+    # micro-batch (fewer, larger GEMMs and launches), then less memory
+    t_best = min(c[0] for c in cands)
+    ties = [c for c in cands if c[0] <= t_best * 1.01]
+    return min(ties, key=lambda c: c[1:5])[5]
 
 
 def plan_from_config(cfg, world):
