@@ -5,6 +5,8 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 #include <stdint.h>
+#include <string>
+#include <stdexcept>
 #include <vector>
 
 namespace py = pybind11;
@@ -73,6 +75,15 @@ int fx_softmax_bwd(int, const void*, const void*, void*, long, int, int, float, 
 int fx_gemm(int, int, int, int, int, int, int, const void*, long, const void*, long, void*, long,
             const void*, void*, long, int, hipStream_t);
 void fx_gemm_set_variant(int);
+int fx_comm_max_world();
+int fx_comm_max_blocks();
+void* fx_comm_alloc(long);
+int fx_comm_free(void*);
+int fx_comm_ipc_handle(void*, char*);
+void* fx_comm_ipc_open(const char*);
+int fx_comm_ipc_close(void*);
+int fx_comm_allreduce(int, int, const void*, void*, long, int, int, const uint64_t*, unsigned int*,
+                      unsigned int*, long, hipStream_t);
 }
 
 #define P(x) reinterpret_cast<void*>(x)
@@ -242,6 +253,32 @@ PYBIND11_MODULE(_kernels, m) {
                    ldaux, beta, S(st));
   });
   m.def("gemm_set_variant", &fx_gemm_set_variant);
+  // intra-node one-shot all-reduce over IPC-mapped peer memory (comm.hip)
+  m.def("comm_max_world", &fx_comm_max_world);
+  m.def("comm_max_blocks", &fx_comm_max_blocks);
+  m.def("comm_alloc", [](long slot_granules) {
+    return reinterpret_cast<ptr>(fx_comm_alloc(slot_granules));
+  });
+  m.def("comm_free", [](ptr p) { return fx_comm_free(P(p)); });
+  m.def("comm_ipc_handle", [](ptr p) {
+    char h[64];
+    const int r = fx_comm_ipc_handle(P(p), h);
+    if (r != 0) throw std::runtime_error("hipIpcGetMemHandle failed: " + std::to_string(r));
+    return py::bytes(h, 64);
+  });
+  m.def("comm_ipc_open", [](py::bytes h) {
+    std::string s = h;
+    if (s.size() != 64) throw std::runtime_error("IPC handle must be 64 bytes");
+    return reinterpret_cast<ptr>(fx_comm_ipc_open(s.data()));
+  });
+  m.def("comm_ipc_close", [](ptr p) { return fx_comm_ipc_close(P(p)); });
+  m.def("comm_allreduce", [](int dt, int op, ptr in, ptr out, long n, int rank, int world,
+                             std::vector<uint64_t> peers, ptr epochs, ptr err, long slot, ptr st) {
+    if ((int)peers.size() != world) throw std::runtime_error("need one receive base per rank");
+    return fx_comm_allreduce(dt, op, CP(in), P(out), n, rank, world, peers.data(),
+                             reinterpret_cast<unsigned int*>(epochs),
+                             reinterpret_cast<unsigned int*>(err), slot, S(st));
+  });
   m.def("softmax_bwd", [](int dt, ptr y, ptr dy, ptr dx, long rows, int Sq, int Sk, float scale,
                           int causal, ptr st) {
     return fx_softmax_bwd(dt, CP(y), CP(dy), P(dx), rows, Sq, Sk, scale, causal, S(st));

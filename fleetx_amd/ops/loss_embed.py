@@ -17,7 +17,12 @@ from . import _lib
 
 
 def _allreduce(t, op, group):
+    # latency-bound [tokens] fp32 vectors: the one-shot IPC kernel when the mp
+    # group is one node, RCCL otherwise (parallel/comm.py)
     if group is not None and group.nranks > 1:
+        if t.is_cuda:
+            from ..parallel.comm import get_communicator
+            return get_communicator(group).all_reduce(t, op)
         dist.all_reduce(t, op=op, group=group.group)
     return t
 

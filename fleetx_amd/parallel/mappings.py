@@ -32,6 +32,11 @@ def _ws(g):
 
 def _all_reduce(x, g):
     if _ws(g) > 1:
+        if x.is_cuda:
+            # small messages (decode, short sequences) take the one-shot IPC
+            # kernel, large ones RCCL (parallel/comm.py)
+            from .comm import get_communicator
+            return get_communicator(g).all_reduce(x)
         dist.all_reduce(x, group=g.group)
     return x
 

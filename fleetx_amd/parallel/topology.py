@@ -254,6 +254,8 @@ def set_hcg(hcg):
 def reset_hcg():
     global _HCG
     _HCG = None
+    from . import comm
+    comm.reset()
 
 
 def mp_group():

@@ -1,0 +1,89 @@
+"""One-shot IPC all-reduce (csrc/kernels/comm.hip, parallel/comm.py) on the GPU.
+
+Two ranks share the one MI355X (IPC handles of the same device opened by the
+peer process; the handle exchange runs over gloo).  Each rank's result is
+compared against an fp32 torch reduction of every rank's input computed
+locally from the shared seed: sum and max, fp32 / bf16 / fp16, sizes from one
+element to the slot limit, many back-to-back calls (epoch parity), out of
+place, and inside a captured HIP graph replayed with new data."""
+import pytest
+import torch
+
+from tests import dist_utils
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(world, n, dtype, it):
+    g = torch.Generator().manual_seed(1000 * it + n)
+    return [torch.randn(n, generator=g).to(dtype) for _ in range(world)]
+
+
+def _oneshot(rank, world):
+    import torch.distributed as dist
+    from fleetx_amd.parallel.comm import IpcAllReduce
+    torch.cuda.set_device(0)
+    ar = IpcAllReduce(None, max_bytes=64 * 1024)
+    worst = {}
+    it = 0
+    for dtype in (torch.float32, torch.bfloat16, torch.float16):
+        for n in (1, 2, 3, 255, 1024, 4097, 16384 if dtype == torch.float32 else 32768):
+            for op in (dist.ReduceOp.SUM, dist.ReduceOp.MAX):
+                it += 1
+                xs = _inputs(world, n, dtype, it)
+                x = xs[rank].cuda()
+                y = ar.all_reduce(x.clone(), op)
+                ref = torch.stack([t.float() for t in xs])
+                ref = ref.sum(0) if op == dist.ReduceOp.SUM else ref.max(0).values
+                err = (y.float().cpu() - ref).abs().max().item()
+                key = (str(dtype), int(op == dist.ReduceOp.MAX))
+                worst[key] = max(worst.get(key, 0.0), err)
+    # out of place, 200 back-to-back calls without host syncs
+    acc = []
+    for i in range(200):
+        x = torch.full((777,), float(rank + i), device="cuda")
+        out = torch.empty_like(x)
+        ar.all_reduce(x, out=out)
+        acc.append(out[0:1])
+    seq = torch.cat(acc).cpu()
+    expect = torch.tensor([float(sum(r + i for r in range(world))) for i in range(200)])
+    # graph capture: the epochs live on the device, so replays keep working
+    static = torch.zeros(4096, device="cuda")
+    ar.all_reduce(static.clone())
+    torch.cuda.synchronize()
+    dist.barrier()
+    gr = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(gr, stream=s):
+            res = ar.all_reduce(static.clone())
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    dist.barrier()
+    graph_ok = []
+    for i in range(5):
+        static.fill_(float(10 * i + rank))
+        gr.replay()
+        torch.cuda.synchronize()
+        graph_ok.append(float(res[123].item()))
+    ar.check()
+    torch.cuda.synchronize()
+    dist.barrier()
+    ar.close()
+    return worst, bool(torch.equal(seq, expect)), graph_ok
+
+
+def test_oneshot_allreduce_two_ranks_one_gpu():
+    res = dist_utils.run(_oneshot, 2, timeout=300)
+    for worst, seq_ok, graph in res:
+        assert seq_ok
+        assert graph == [float(sum(10 * i + r for r in range(2))) for i in range(5)]
+        for (dt, is_max), e in worst.items():
+            if is_max:
+                assert e == 0.0, (dt, e)
+            else:
+                tol = 1e-6 if "float32" in dt else (0.07 if "bfloat16" in dt else 0.01)
+                assert e <= tol, (dt, e)
+    # all ranks see bitwise-identical results
+    assert res[0][0] == res[1][0]

@@ -101,3 +101,21 @@ LAYOUTS = {
 def test_layout_matches_single_rank_on_gpu(ref_gpu, name):
     out = dist_utils.run(_train_gpu, 2, LAYOUTS[name], timeout=300)
     _check(out, ref_gpu)
+
+
+def _train_gpu_oneshot(rank, world, layout):
+    # the TP activation / cross-entropy all-reduces of this small model all fit
+    # the one-shot IPC kernel (parallel/comm.py); gloo only exchanges handles
+    os.environ["FLEETX_ONESHOT_FORCE"] = "1"
+    res = _train_gpu(rank, world, layout)
+    from fleetx_amd.parallel import comm
+    res["oneshot_calls"] = sum(c.oneshot.calls for c in comm._COMMS.values()
+                               if c.oneshot is not None)
+    return res
+
+
+@pytest.mark.parametrize("name", ["tp2", "tp2_sp"])
+def test_tp_oneshot_allreduce_matches_single_rank(ref_gpu, name):
+    out = dist_utils.run(_train_gpu_oneshot, 2, LAYOUTS[name], timeout=300)
+    assert all(r["oneshot_calls"] > 0 for r in out), [r["oneshot_calls"] for r in out]
+    _check(out, ref_gpu)
