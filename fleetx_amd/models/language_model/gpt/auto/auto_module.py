@@ -17,10 +17,11 @@ import copy
 
 from .....parallel import topology as topo
 from .....parallel.auto.mesh import Mesh, shard_tensor, verify_annotations
+from .....parallel.auto.partition import lower
 from .....utils.log import logger
 from ...language_module import GPTModule
 from ...utils import process_data_configs
-from ..model import GPTPretrainingCriterion
+from ..model import GPTForPretraining, GPTPretrainingCriterion
 
 
 class GPTPretrainingCriterionAuto(GPTPretrainingCriterion):
@@ -30,10 +31,14 @@ class GPTPretrainingCriterionAuto(GPTPretrainingCriterion):
 
 
 def annotate_gpt(model, mesh):
-    """Reference shard specs (``auto_model.py``) on the built GPT network."""
+    """Reference shard specs (``auto_model.py``) on the built GPT network:
+    QKV / FFN1 ``[None, mp]``, out-proj / FFN2 ``[mp, None]``, word embedding
+    ``[mp, None]``, and every decoder layer placed on its pipeline sub-mesh
+    ``mesh[stage]`` (``auto_model.py:601-610``)."""
     pm = mesh.process_mesh
     mp = mesh.mp
     n = 0
+    num_layers = None
     for name, mod in model.named_modules():
         w = getattr(mod, "weight", None)
         if w is None or w.dim() != 2:
@@ -47,6 +52,13 @@ def annotate_gpt(model, mesh):
         else:
             continue
         n += 1
+    layers = getattr(getattr(model, "gpt", None), "layers", None)
+    if layers is not None:
+        num_layers = len(layers)
+        stages = mesh.stages(num_layers)
+        for i, layer in enumerate(layers):
+            layer._fx_stage = stages[i]
+            layer._fx_mesh = mesh[stages[i]]
     return n
 
 
@@ -61,12 +73,35 @@ class GPTModuleAuto(GPTModule):
         process_data_configs(configs)
         return configs
 
+    def _serial_model(self):
+        """The annotated serial network (whole weights, one-rank mp world)."""
+        cfg = copy.deepcopy(self.gpt_config)
+        cfg.sequence_parallel = False
+        with topo.serial_scope():
+            serial = GPTForPretraining(cfg)
+        annotate_gpt(serial, self.mesh)
+        return serial
+
     def get_model(self):
         model = super().get_model()
-        n = annotate_gpt(model, self.mesh)
-        checked = verify_annotations(model)
-        logger.info("auto-parallel mesh %s: %d annotated weights (%d verified against TP layers)"
-                    % (self.mesh.process_mesh, n, checked))
+        q = self.configs.get("Quantization")
+        if q is not None and q.get("enable", False):
+            # QAT wraps the layers: keep the runtime's own partitioning, check it
+            n = annotate_gpt(model, self.mesh)
+            checked = verify_annotations(model)
+            logger.info("auto-parallel mesh %s: %d annotated weights (%d verified, QAT)"
+                        % (self.mesh.process_mesh, n, checked))
+            return model
+        # semi-auto lowering: the annotations of the serial network decide how
+        # every tensor is split (parallel/auto/partition.py)
+        serial = self._serial_model()
+        layout = lower(serial, model, self.mesh)
+        self.auto_layout = layout
+        logger.info("auto-parallel mesh %s: lowered %d tensors from the annotated serial network "
+                    "(tensor parallel over %s x%d, %d layers stage-annotated)"
+                    % (self.mesh.process_mesh, layout["lowered"], layout["tp_dim"],
+                       layout["tp_degree"], len(layout["stages"])))
+        del serial
         return model
 
     def get_loss_fn(self):

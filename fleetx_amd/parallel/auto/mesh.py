@@ -6,12 +6,13 @@ mp]`` with degree-1 axes dropped, ``mesh[stage]`` sub-meshes,
 ``stages(num_layers)``), and ``auto.shard_tensor`` / ``auto.shard_op``
 annotations (``auto_model.py:109-110,143-146,238-239,384-387,464-465,601-610``).
 
-Annotations are recorded on tensors as ``_fx_dist = (mesh, spec)`` and
-checked against how the layer is actually partitioned when the model is
-materialised: a spec ``[None, "mp"]`` on a ``[in, out]`` weight means a
-column-parallel split, ``["mp", None]`` a row-parallel split.  The execution
-itself is the explicit hybrid runtime (TP layers, 1F1B pipeline, flat-buffer
-DP/ZeRO) — there is no graph partitioner to complete specs.
+Annotations are recorded on tensors as ``_fx_dist = (mesh, spec)``: a spec
+``[None, "mp"]`` on a ``[in, out]`` weight means a column-parallel split,
+``["mp", None]`` a row-parallel split.  :mod:`.partition` completes the specs
+of a serial network and lowers them: every tensor of the materialised hybrid
+model (TP layers, 1F1B stages, flat-buffer DP/ZeRO) is the slice of the
+serial tensor its spec names.  :func:`verify_annotations` checks annotations
+made directly on an already-parallel model (the QAT path).
 """
 import numpy as np
 
@@ -43,6 +44,8 @@ class ProcessMesh:
 
     def __getitem__(self, idx):
         sub = self.mesh[idx]
+        if np.ndim(sub) == 0:  # a single process: a one-process mesh
+            return ProcessMesh([int(sub)], ["serial"])
         return ProcessMesh(sub, self.dim_names[1:] if np.ndim(sub) == self.mesh.ndim - 1
                            else self.dim_names)
 

@@ -22,8 +22,7 @@ from . import topology as topo
 
 
 def _grp():
-    g = topo.get_hcg().get_model_parallel_group()
-    return g
+    return topo.mp_group()  # None inside topology.serial_scope()
 
 
 def _ws(g):

@@ -258,16 +258,33 @@ def reset_hcg():
     comm.reset()
 
 
+_SERIAL = [0]
+
+
+class serial_scope:
+    """Layers built inside see a single-rank model-parallel world (full,
+    unsplit weights): the semi-auto front end builds the serial network this
+    way and partitions it from its shard annotations (parallel/auto/partition.py)."""
+
+    def __enter__(self):
+        _SERIAL[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _SERIAL[0] -= 1
+        return False
+
+
 def mp_group():
-    return get_hcg().get_model_parallel_group()
+    return None if _SERIAL[0] else get_hcg().get_model_parallel_group()
 
 
 def mp_world_size():
-    return get_hcg().mp_degree if _HCG is not None else 1
+    return get_hcg().mp_degree if _HCG is not None and not _SERIAL[0] else 1
 
 
 def mp_rank():
-    return get_hcg().mp_rank if _HCG is not None else 0
+    return get_hcg().mp_rank if _HCG is not None and not _SERIAL[0] else 0
 
 
 def init_distributed(backend=None, timeout_s=1800):

@@ -80,3 +80,90 @@ def _auto_full_worker(rank, world, tmp):
 def test_auto_full_gloo_world2(tmp_path):
     from tests.dist_utils import run
     run(_auto_full_worker, 2, str(tmp_path))
+
+
+def _lowering_worker(rank, world, mp, pp, bad):
+    """Semi-auto lowering: the per-rank model equals the annotated serial
+    network split by its specs (gathered shards == serial weights, gathered
+    vocab-parallel logits == serial logits); a wrong annotation is refused."""
+    import torch.distributed as dist
+    from fleetx_amd.utils import config as cfgmod
+    from fleetx_amd.utils import env
+    from fleetx_amd.models import build_module
+    from fleetx_amd.models.language_model.gpt.auto import auto_module as am
+    from fleetx_amd.parallel import topology as topo
+    topo.reset_hcg()
+    ov = TINY + ["Distributed.mp_degree=%d" % mp, "Distributed.pp_degree=%d" % pp,
+                 "Distributed.dp_degree=1", "Model.hidden_dropout_prob=0.0",
+                 "Model.attention_probs_dropout_prob=0.0", "Global.global_batch_size=4"]
+    cfg = cfgmod.get_auto_config(os.path.join(AUTO, "pretrain_gpt_345M_single_card.yaml"),
+                                 overrides=ov, show=False)
+    env.init_dist_env(cfg)
+    env.set_seed(cfg.Global.seed)
+    if bad:
+        orig = am.annotate_gpt
+
+        def wrong(model, mesh):
+            n = orig(model, mesh)
+            for name, mod in model.named_modules():
+                if name.endswith("fc1"):
+                    shard_tensor(mod.weight, mesh.process_mesh, ["mp", None])  # row, not column
+            return n
+        am.annotate_gpt = wrong
+        try:
+            build_module(cfg).get_model()
+        except ValueError as e:
+            return {"refused": str(e)}
+        finally:
+            am.annotate_gpt = orig
+        return {"refused": None}
+    module = build_module(cfg)
+    model = module.get_model()
+    serial = module._serial_model()
+    hcg = topo.get_hcg()
+    out = {"layout": {k: v for k, v in module.auto_layout.items() if k != "stages"},
+           "nstages": len(module.auto_layout["stages"])}
+    if mp > 1:
+        w = model.gpt.layers[0].mlp.fc1.weight.detach()
+        parts = [torch.empty_like(w) for _ in range(mp)]
+        dist.all_gather(parts, w.contiguous())
+        out["fc1_ok"] = torch.equal(torch.cat(parts, 0), serial.gpt.layers[0].mlp.fc1.weight)
+        w2 = model.gpt.layers[1].attn.out_proj.weight.detach()
+        parts = [torch.empty_like(w2) for _ in range(mp)]
+        dist.all_gather(parts, w2.contiguous())
+        out["out_ok"] = torch.equal(torch.cat(parts, 1), serial.gpt.layers[1].attn.out_proj.weight)
+        model.eval()
+        serial.eval()
+        toks = torch.randint(0, 128, (2, 16), generator=torch.Generator().manual_seed(3))
+        with torch.no_grad():
+            lg = model(toks)
+            parts = [torch.empty_like(lg) for _ in range(mp)]
+            dist.all_gather(parts, lg.contiguous())
+            with topo.serial_scope():
+                ref = serial(toks)
+        out["logit_err"] = (torch.cat(parts, -1) - ref).abs().max().item()
+    else:
+        # pipeline: every stage holds exactly its annotated layers' serial weights
+        names = [n for n, _ in model.named_parameters()]
+        out["n_params"] = len(names)
+        out["stage"] = hcg.pp_rank
+    return out
+
+
+@pytest.mark.parametrize("mp,pp", [(2, 1), (1, 2)])
+def test_semi_auto_lowering_matches_serial(mp, pp):
+    from tests.dist_utils import run
+    res = run(_lowering_worker, 2, mp, pp, False)
+    for r in res:
+        assert r["layout"]["tp_degree"] == mp and r["layout"]["lowered"] > 0
+        assert r["nstages"] == 2
+        if mp > 1:
+            assert r["fc1_ok"] and r["out_ok"]
+            assert r["logit_err"] < 1e-4, r["logit_err"]
+
+
+def test_semi_auto_wrong_annotation_refused():
+    from tests.dist_utils import run
+    res = run(_lowering_worker, 2, 2, 1, True)
+    for r in res:
+        assert r["refused"] and "fc1" in r["refused"], r
