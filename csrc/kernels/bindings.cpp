@@ -75,6 +75,9 @@ int fx_softmax_bwd(int, const void*, const void*, void*, long, int, int, float, 
 int fx_gemm(int, int, int, int, int, int, int, const void*, long, const void*, long, void*, long,
             const void*, void*, long, int, hipStream_t);
 void fx_gemm_set_variant(int);
+int fx_decode_gemv(int, int, int, int, int, const void*, long, const void*, long, const void*,
+                   const void*, long, void*, long, void*, void*, const long*, int, int, int,
+                   hipStream_t);
 int fx_comm_max_world();
 int fx_comm_max_blocks();
 void* fx_comm_alloc(long);
@@ -253,6 +256,14 @@ PYBIND11_MODULE(_kernels, m) {
                    ldaux, beta, S(st));
   });
   m.def("gemm_set_variant", &fx_gemm_set_variant);
+  // decode-time skinny GEMM with fused sub-layer epilogues (decode_gemv.hip)
+  m.def("decode_gemv", [](int dt, int epi, int M, int N, int K, ptr x, long ldx, ptr w, long ldw,
+                          ptr bias, ptr res, long ldres, ptr y, long ldy, ptr kc, ptr vc, ptr pos,
+                          int heads, int head_dim, int maxlen, ptr st) {
+    return fx_decode_gemv(dt, epi, M, N, K, CP(x), ldx, CP(w), ldw, CP(bias), CP(res), ldres, P(y),
+                          ldy, P(kc), P(vc), reinterpret_cast<const long*>(pos), heads, head_dim,
+                          maxlen, S(st));
+  });
   // intra-node one-shot all-reduce over IPC-mapped peer memory (comm.hip)
   m.def("comm_max_world", &fx_comm_max_world);
   m.def("comm_max_blocks", &fx_comm_max_blocks);

@@ -66,7 +66,8 @@ template <typename T, int D>
 __global__ __launch_bounds__(256) void decode_attn_split_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int* __restrict__ lens, float* __restrict__ ws,
-    int H, int nsplit, int chunk, long sqb, long sqh, long skb, long sks, long skh, float scale) {
+    int H, int nsplit, int chunk, long sqb, long sqh, long skb, long sks, long skh, float scale,
+    uint16_t* __restrict__ out, long sob) {
   constexpr int LPK = D / 8;        // lanes per key row
   constexpr int KPW = 64 / LPK;     // key rows per wave instruction
   constexpr int U = 4;              // key rows per lane group per step
@@ -149,6 +150,14 @@ __global__ __launch_bounds__(256) void decode_attn_split_kernel(
         for (int j = 0; j < 8; ++j) O[j] += sm_o[t][j] * a;
       }
     }
+    if (nsplit == 1) {  // one split: normalise and store the output directly
+      const float inv = L > 0.f ? 1.f / L : 0.f;
+      float r[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = O[j] * inv;
+      store8<T>(out + b * sob + hd * D + threadIdx.x * 8, r);
+      return;
+    }
     float* wp = ws + (long)blockIdx.x * (D + 2);
 #pragma unroll
     for (int j = 0; j < 8; ++j) wp[threadIdx.x * 8 + j] = O[j];
@@ -215,8 +224,9 @@ extern "C" int fx_decode_attn(int dt, const void* q, const void* kc, const void*
   do {                                                                                           \
     decode_attn_split_kernel<TT, DD><<<g, 256, 0, st>>>(                                         \
         (const uint16_t*)q, (const uint16_t*)kc, (const uint16_t*)vc, lens, ws, H, nsplit, chunk, \
-        sqb, sqh, skb, sks, skh, scale);                                                         \
-    decode_attn_combine_kernel<TT, DD><<<B * H, DD, 0, st>>>(ws, (uint16_t*)out, H, nsplit, sob); \
+        sqb, sqh, skb, sks, skh, scale, (uint16_t*)out, sob);                                     \
+    if (nsplit > 1)                                                                              \
+      decode_attn_combine_kernel<TT, DD><<<B * H, DD, 0, st>>>(ws, (uint16_t*)out, H, nsplit, sob); \
   } while (0)
   if (dt == 0) {
     if (D == 128) FX_DEC(bf16, 128); else FX_DEC(bf16, 64);

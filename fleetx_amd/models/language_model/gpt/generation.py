@@ -169,6 +169,38 @@ def _layer_decode(layer, x, cache, li, pos, lens_after):
     return ops.bias_dropout_add(m, mb, x2)
 
 
+def _fusable(layer):
+    from ....parallel import layers as L
+    a, m = layer.attn, layer.mlp
+    return (topo.mp_world_size() == 1 and type(a.qkv_proj) is L.ColumnParallelLinear
+            and type(a.out_proj) is L.RowParallelLinear and type(m.fc1) is L.ColumnParallelLinear
+            and type(m.fc2) is L.RowParallelLinear)
+
+
+def _layer_decode_fused(layer, x, cache, li, pos, lens_after):
+    """One-token pass as five kernels (K19, the fused_multi_transformer
+    counterpart): LN1 -> [QKV GEMV + bias, K/V appended to the cache in the
+    epilogue] -> split-K decode attention -> [out-proj GEMV + bias + residual]
+    -> LN2 -> [FFN1 GEMV + bias + GeLU] -> [FFN2 GEMV + bias + residual].
+    Returns None when a GEMV does not cover the shape (batch > 16)."""
+    from ....ops import gemm as G
+    attn, mlp = layer.attn, layer.mlp
+    B, h = x.shape[0], x.shape[-1]
+    x2d = x.reshape(B, h)
+    hn = layer.ln1(x2d)
+    q = G.decode_linear(hn, attn.qkv_proj.weight, attn.qkv_proj.bias, G.GV_QKV,
+                        qkv_cache=(cache.k[li], cache.v[li], pos))
+    if q is None:
+        return None
+    o = ops.decode_attention(q.view(B, attn.heads, attn.head_dim), cache.k[li], cache.v[li],
+                             lens_after)
+    x2 = G.decode_linear(o.view(B, -1), attn.out_proj.weight, attn.out_proj.bias, G.GV_RES,
+                         res=x2d)
+    f = G.decode_linear(layer.ln2(x2), mlp.fc1.weight, mlp.fc1.bias, G.GV_GELU)
+    out = G.decode_linear(f, mlp.fc2.weight, mlp.fc2.bias, G.GV_RES, res=x2)
+    return out.view(B, 1, h)
+
+
 class _GraphedDecodeStep:
     """The per-token decode step (embedding -> L decoder layers against the KV
     cache -> final LN -> logits) captured once into a HIP graph and replayed
@@ -231,6 +263,8 @@ class GPTForGeneration(torch.nn.Module):
         self.forced_eos_token_id = c.get("forced_eos_token_id")
         self.num_return_sequences = c.get("num_return_sequences", 1)
         self.use_hip_graph = bool(c.get("use_hip_graph", True))
+        # decode layers as five fused kernels with weight-streaming GEMVs (K19)
+        self.fused_decode = bool(c.get("fused_decode", True))
         if self.decode_strategy not in ("sampling", "greedy_search"):
             raise ValueError("decode_strategy must be sampling or greedy_search")
 
@@ -256,14 +290,22 @@ class GPTForGeneration(torch.nn.Module):
                           cur[:, None], self.gpt.embeddings.position_embeddings, 0) \
             if topo.mp_world_size() == 1 else self.gpt.embeddings(nxt[:, None], cur[:, None])
         after = (cur + 1).to(torch.int32)
+        fused = self.fused_decode and x.is_cuda and x.shape[0] <= 16
         for li, layer in enumerate(self.gpt.layers):
-            x = _layer_decode(layer, x, cache, li, cur, after)
+            y = _layer_decode_fused(layer, x, cache, li, cur, after) \
+                if fused and _fusable(layer) else None
+            x = y if y is not None else _layer_decode(layer, x, cache, li, cur, after)
         x = self.gpt.final_ln(x)
         return self._logits(x[:, 0])
 
     def _logits(self, h):
         w = self.gpt.embeddings.word_embeddings.weight
-        logits = F.linear(h, w)
+        logits = None
+        if self.fused_decode and topo.mp_world_size() == 1:
+            from ....ops import gemm as G
+            logits = G.decode_linear(h.contiguous(), w)
+        if logits is None:
+            logits = F.linear(h, w)
         if topo.mp_world_size() > 1:
             logits = M.gather_from_mp(logits)
         return logits.float()

@@ -218,9 +218,11 @@ def flash_attention_qkvpacked(qkv, causal=True, dropout_p=0.0, key=0, scale=None
     return _PackedEntry.apply(qkv, causal, float(dropout_p), key, scale, kv_lens, key_bias)
 
 
-def decode_splits(B, H, maxlen, target_wgs=2048, min_chunk=128):
+def decode_splits(B, H, maxlen, target_wgs=2048, min_chunk=512):
     """Split-K factor for decode attention: enough workgroups to cover the 256
-    CUs about eight deep (measured: 512 WGs reach 3.2 TB/s, >=1024 5.3 TB/s), at least ``min_chunk`` keys per split."""
+    CUs about eight deep (measured: 512 WGs reach 3.2 TB/s, >=1024 5.3 TB/s), at least
+    ``min_chunk`` keys per split (a single split writes the output directly:
+    short-context decode runs one kernel, no combine pass)."""
     n = max(1, -(-target_wgs // max(1, B * H)))
     return max(1, min(n, -(-maxlen // min_chunk)))
 

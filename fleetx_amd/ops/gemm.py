@@ -156,3 +156,53 @@ def wgrad_16(dy2, x2):
     rc = _launch(_lib.dt_code(dy2.dtype), LAY_MC, LAY_MC, EPI_STORE, N, K, M, dy2, dy2.stride(0),
                  x2, x2.stride(0), out, K)
     return out if rc == 0 else None
+
+
+# ----------------------------------------------------------------------------
+# decode-time skinny GEMM (csrc/kernels/decode_gemv.hip)
+# ----------------------------------------------------------------------------
+GV_BIAS, GV_GELU, GV_RES, GV_QKV = range(4)
+
+
+def decode_linear(x, weight, bias=None, epi=GV_BIAS, res=None, qkv_cache=None):
+    """``x [M, K] @ weight[N, K]^T`` for M <= 16 rows on the weight-streaming
+    MFMA GEMV, with the epilogue ``epi``: GV_BIAS (+b), GV_GELU (gelu_tanh(+b)),
+    GV_RES (+b + res[M, N]) or GV_QKV (``qkv_cache = (k_cache, v_cache, pos)``:
+    the packed [heads][3][head_dim] output is scattered -- q returned as [M, H*D],
+    k/v written into the caches [M, maxlen, H, D] at ``pos`` [M]).
+
+    Returns the output, or None when the kernel does not cover the shape (the
+    caller then uses the general GEMM)."""
+    if not x.is_cuda or x.dim() != 2 or x.shape[0] > 16 or x.dtype not in (torch.bfloat16,
+                                                                            torch.float16):
+        return None
+    M, K = x.shape
+    N = weight.shape[0]
+    if epi == GV_BIAS and bias is None and N * K > 48 * 2 ** 20:
+        # a plain product of a large weight (e.g. the LM head): hipBLASLt streams
+        # it faster (tools/bench_gemv.py), and there is no epilogue to fuse
+        return None
+    if weight.dtype != x.dtype or weight.stride(1) != 1 or x.stride(1) != 1 or K % 1024:
+        return None
+    k = _lib.kernels()
+    kc = vc = pos = None
+    heads = hd = maxlen = 0
+    if epi == GV_QKV:
+        kc, vc, pos = qkv_cache
+        maxlen, heads, hd = kc.shape[1], kc.shape[2], kc.shape[3]
+        assert N == 3 * heads * hd and kc.is_contiguous() and vc.is_contiguous()
+        assert pos.dtype == torch.int64 and pos.numel() == M
+        y = torch.empty(M, heads * hd, device=x.device, dtype=x.dtype)
+    else:
+        y = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    if res is not None:
+        assert res.shape == (M, N) and res.stride(1) == 1
+    nb = k.decode_gemv(_lib.dt_code(x.dtype), int(epi), M, N, K, x.data_ptr(), x.stride(0),
+                       weight.data_ptr(), weight.stride(0), _lib.ptr(bias), _lib.ptr(res),
+                       res.stride(0) if res is not None else 0, y.data_ptr(), y.stride(0),
+                       _lib.ptr(kc), _lib.ptr(vc), _lib.ptr(pos), heads, hd, maxlen,
+                       _lib.stream())
+    if nb == 0:
+        return None
+    _lib.maybe_sync()
+    return y
