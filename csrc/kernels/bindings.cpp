@@ -78,6 +78,8 @@ void fx_gemm_set_variant(int);
 int fx_decode_gemv(int, int, int, int, int, const void*, long, const void*, long, const void*,
                    const void*, long, void*, long, void*, void*, const long*, int, int, int,
                    hipStream_t);
+void fx_set_dropout_salt(const void*);
+void fx_set_adamw_lr_ptr(const void*);
 int fx_comm_max_world();
 int fx_comm_max_blocks();
 void* fx_comm_alloc(long);
@@ -264,6 +266,9 @@ PYBIND11_MODULE(_kernels, m) {
                           ldy, P(kc), P(vc), reinterpret_cast<const long*>(pos), heads, head_dim,
                           maxlen, S(st));
   });
+  // graph mode: device-resident dropout salt / AdamW learning rate (0 = off)
+  m.def("set_dropout_salt", [](ptr p) { fx_set_dropout_salt(CP(p)); });
+  m.def("set_adamw_lr_ptr", [](ptr p) { fx_set_adamw_lr_ptr(CP(p)); });
   // intra-node one-shot all-reduce over IPC-mapped peer memory (comm.hip)
   m.def("comm_max_world", &fx_comm_max_world);
   m.def("comm_max_blocks", &fx_comm_max_blocks);

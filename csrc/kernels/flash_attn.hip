@@ -181,7 +181,20 @@ struct AttnParams {
   float scale;
   uint32_t klo, khi, thr;
   float drop_scale;
+  const uint64_t* salt;  // graph mode: per-replay device salt (fx_set_dropout_salt)
 };
+
+// per-(batch, head) dropout hash seed; under graph mode the baked key is
+// re-keyed by the device salt first
+__device__ __forceinline__ uint32_t attn_cb(const AttnParams& P, int bh) {
+  uint32_t klo = P.klo, khi = P.khi;
+  if (P.salt != nullptr) {
+    const uint64_t k = salt_key(((uint64_t)khi << 32) | klo, *P.salt);
+    klo = (uint32_t)k;
+    khi = (uint32_t)(k >> 32);
+  }
+  return lowbias32((uint32_t)bh ^ khi) ^ klo;
+}
 
 // S^T tile rows are keys: register i of lane half h holds key crow(i, h) of
 // its 32-row block.  Keys crow(4g..4g+3, h) = 8g + 4h + {0..3} are contiguous,
@@ -274,7 +287,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
     for (int i = 0; i < 16; ++i) oacc[dt][i] = 0.f;
   float m_run = -INFINITY, lsum = 0.f;
   const float sl2 = P.scale * LOG2E;
-  const uint32_t cb = DROP ? (lowbias32((uint32_t)bh ^ P.khi) ^ P.klo) : 0u;
+  const uint32_t cb = DROP ? attn_cb(P, bh) : 0u;
 
   GldsStream<D, KV> kld, vld;
   kld.init(kp, P.sk_s, kv_end, w, lane);
@@ -465,7 +478,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
   const float lse2 = qvalid ? P.lse[(long)bh * P.Sq + qi] * LOG2E : INFINITY;
   const float dlt = qvalid ? P.delta[(long)bh * P.Sq + qi] : 0.f;
   const float sl2 = P.scale * LOG2E;
-  const uint32_t cb = DROP ? (lowbias32((uint32_t)bh ^ P.khi) ^ P.klo) : 0u;
+  const uint32_t cb = DROP ? attn_cb(P, bh) : 0u;
 
   int kv_end = kv_len;
   if (CAUSAL) kv_end = min(kv_end, (qblock + 1) * 128);
@@ -627,7 +640,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) dkacc[dt][i] = dvacc[dt][i] = 0.f;
   const float sl2 = P.scale * LOG2E;
-  const uint32_t cb = DROP ? (lowbias32((uint32_t)bh ^ P.khi) ^ P.klo) : 0u;
+  const uint32_t cb = DROP ? attn_cb(P, bh) : 0u;
 
   const int q_begin = CAUSAL ? (kblock * 128 / QT) * QT : 0;
   const int ntiles = P.Sq > q_begin ? (P.Sq - q_begin + QT - 1) / QT : 0;
@@ -773,6 +786,7 @@ AttnParams make_params(const void* q, const void* k, const void* v, const long* 
   P.khi = (uint32_t)(key >> 32);
   P.thr = (uint32_t)(p * 65536.0f + 0.5f);
   P.drop_scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  P.salt = p > 0.f ? g_fx_dropout_salt : nullptr;
   return P;
 }
 

@@ -92,6 +92,17 @@ __device__ __forceinline__ uint32_t elem_rand_pair(uint64_t i, uint32_t klo, uin
   return lowbias32((uint32_t)pair ^ c);
 }
 
+// splitmix64 finaliser: graph-mode re-keying of dropout streams
+__host__ __device__ __forceinline__ uint64_t fx_mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+extern const uint64_t* g_fx_dropout_salt;  // host-side, set by fx_set_dropout_salt
+__device__ __forceinline__ uint64_t salt_key(uint64_t key, uint64_t salt) {
+  return fx_mix64(key ^ fx_mix64(salt + 0x9E3779B97F4A7C15ull)) & 0x7FFFFFFFFFFFFFFFull;
+}
+
 // Round-trip through the 16-bit storage type (what a store + reload would see).
 template <typename T>
 __device__ __forceinline__ float round_to(float f) {

@@ -156,8 +156,9 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(
     float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
     float* __restrict__ v, uint16_t* __restrict__ p16, long n, float lr, float beta1,
     float beta2, float eps, float wd, float l2, const float* __restrict__ gscale,
-    const int* __restrict__ skip, const int* __restrict__ step) {
+    const int* __restrict__ skip, const int* __restrict__ step, const float* __restrict__ lr_dev) {
   if (skip && *skip) return;
+  if (lr_dev != nullptr) lr = *lr_dev;  // graph mode: the scheduler's lr lives on the device
   const float gs = gscale ? *gscale : 1.f;
   const float t = (float)(*step);
   const float bc1 = 1.f - __powf(beta1, t);
@@ -359,6 +360,8 @@ extern "C" void fx_sumsq_f32(const float* x, long n, float* partial, int blocks,
 }
 
 static int g_adamw_grid = 0, g_adamw_nt = 1;  // tuning knobs (tools/bench_optim.py)
+static const float* g_adamw_lr = nullptr;     // graph mode: device learning rate
+extern "C" void fx_set_adamw_lr_ptr(const void* p) { g_adamw_lr = (const float*)p; }
 extern "C" void fx_adamw_tune(int grid, int nt) {
   g_adamw_grid = grid;
   g_adamw_nt = nt;
@@ -376,11 +379,11 @@ extern "C" void fx_adamw_flat(int dtype, float* p, const float* g, float* m, flo
   if (g_adamw_nt) {
     FX_DISPATCH_T(dtype, adamw_flat_kernel<T, true><<<grid, 256, 0, st>>>(
                              p, g, m, v, (uint16_t*)p16, n, lr, beta1, beta2, eps, wd, l2,
-                             gscale, skip, step));
+                             gscale, skip, step, g_adamw_lr));
   } else {
     FX_DISPATCH_T(dtype, adamw_flat_kernel<T, false><<<grid, 256, 0, st>>>(
                              p, g, m, v, (uint16_t*)p16, n, lr, beta1, beta2, eps, wd, l2,
-                             gscale, skip, step));
+                             gscale, skip, step, g_adamw_lr));
   }
 }
 

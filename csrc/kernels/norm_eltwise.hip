@@ -20,7 +20,20 @@ struct DropCfg {
   uint32_t klo, khi, thr;  // drop when rand16 < thr
   float scale;             // 1/(1-p)
   int enabled;
+  const uint64_t* salt;    // graph mode: per-replay device salt mixed into the key
 };
+
+// Graph mode (fx_set_dropout_salt): the key baked into a captured launch is
+// re-keyed on the device by the step salt, so every replay draws new masks
+// while forward, backward and recompute of one step agree.
+__device__ __forceinline__ DropCfg resolve_drop(DropCfg d) {
+  if (d.enabled && d.salt != nullptr) {
+    const uint64_t k = salt_key(((uint64_t)d.khi << 32) | d.klo, *d.salt);
+    d.klo = (uint32_t)k;
+    d.khi = (uint32_t)(k >> 32);
+  }
+  return d;
+}
 
 __device__ __forceinline__ float drop_apply(float v, uint64_t idx, const DropCfg& d) {
   if (!d.enabled) return v;
@@ -40,7 +53,8 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
     const uint16_t* __restrict__ residual, const uint16_t* __restrict__ gamma,
     const uint16_t* __restrict__ beta, uint16_t* __restrict__ s_out,
     uint16_t* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
-    int rows, int h, float eps, DropCfg drop) {
+    int rows, int h, float eps, DropCfg drop_) {
+  const DropCfg drop = resolve_drop(drop_);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -110,7 +124,8 @@ __global__ __launch_bounds__(256) void add_ln_fwd_generic(
     const uint16_t* __restrict__ residual, const uint16_t* __restrict__ gamma,
     const uint16_t* __restrict__ beta, uint16_t* __restrict__ s_out,
     uint16_t* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
-    int rows, int h, float eps, DropCfg drop) {
+    int rows, int h, float eps, DropCfg drop_) {
+  const DropCfg drop = resolve_drop(drop_);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -170,7 +185,8 @@ __global__ __launch_bounds__(256) void ln_bwd_row_kernel(
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const uint16_t* __restrict__ gamma, const uint16_t* __restrict__ ds_in,
     uint16_t* __restrict__ ds_out, uint16_t* __restrict__ dx_out, int rows, int h,
-    DropCfg drop) {
+    DropCfg drop_) {
+  const DropCfg drop = resolve_drop(drop_);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -223,7 +239,8 @@ __global__ __launch_bounds__(256) void ln_bwd_row_generic(
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const uint16_t* __restrict__ gamma, const uint16_t* __restrict__ ds_in,
     uint16_t* __restrict__ ds_out, uint16_t* __restrict__ dx_out, int rows, int h,
-    DropCfg drop) {
+    DropCfg drop_) {
+  const DropCfg drop = resolve_drop(drop_);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -421,7 +438,8 @@ template <typename T>
 __global__ __launch_bounds__(256) void bias_dropout_add_fwd_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ bias,
     const uint16_t* __restrict__ residual, uint16_t* __restrict__ out, long n8, int cols,
-    DropCfg drop) {
+    DropCfg drop_) {
+  const DropCfg drop = resolve_drop(drop_);
   for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < n8; v += (long)gridDim.x * blockDim.x) {
     const long off = v * 8;
     const int c = (int)(off % cols);
@@ -449,7 +467,8 @@ __global__ __launch_bounds__(256) void bias_dropout_add_fwd_kernel(
 template <typename T>
 __global__ __launch_bounds__(256) void dropout_bwd_colsum_kernel(
     const uint16_t* __restrict__ dout, uint16_t* __restrict__ dx, float* __restrict__ part,
-    int rows, int cols, int rows_per_split, DropCfg drop) {
+    int rows, int cols, int rows_per_split, DropCfg drop_) {
+  const DropCfg drop = resolve_drop(drop_);
   __shared__ float red[16][129];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int col = blockIdx.x * 128 + tx * 8;
@@ -490,7 +509,8 @@ __global__ __launch_bounds__(256) void dropout_bwd_colsum_kernel(
 template <typename T>
 __global__ __launch_bounds__(256) void dropout_fwd_kernel(const uint16_t* __restrict__ x,
                                                           uint16_t* __restrict__ y, long n8,
-                                                          DropCfg drop) {
+                                                          DropCfg drop_) {
+  const DropCfg drop = resolve_drop(drop_);
   for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < n8; v += (long)gridDim.x * blockDim.x) {
     const long off = v * 8;
     float a[8];
@@ -508,6 +528,7 @@ DropCfg make_drop(float p, uint64_t key) {
   d.khi = (uint32_t)(key >> 32);
   d.thr = (uint32_t)(p * 65536.0f + 0.5f);
   d.scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  d.salt = g_fx_dropout_salt;
   return d;
 }
 
@@ -688,4 +709,11 @@ extern "C" void fx_dropout_fwd(int dtype, const void* x, void* y, long n, float 
   long n8 = n / 8;
   FX_DISPATCH_T(dtype, dropout_fwd_kernel<T><<<grid_for(n8), 256, 0, st>>>(
                            (const uint16_t*)x, (uint16_t*)y, n8, d));
+}
+
+// graph-mode dropout salt (see resolve_drop): a device uint64 read by every
+// dropout-bearing launch issued while it is set (nullptr = eager keys)
+const uint64_t* g_fx_dropout_salt = nullptr;
+extern "C" void fx_set_dropout_salt(const void* p) {
+  g_fx_dropout_salt = reinterpret_cast<const uint64_t*>(p);
 }

@@ -31,6 +31,7 @@ import torch
 import torch.distributed as dist
 
 from .basic_engine import BasicEngine
+from ...ops import _lib
 from ...optims import build_optimizer, build_lr_scheduler
 from ...parallel import topology as topo
 from ...parallel.grad_buffer import FlatParamGradBuffer
@@ -206,13 +207,17 @@ class EagerEngine(BasicEngine):
                     decr_every=int(amp.get("decr_every_n_nan_or_inf", 2)),
                     device=self.device)
                 self.optimizer.loss_scale = self.scaler.scale
+            # whole-step HIP graph (Engine.cuda_graph): one replay per step
+            self._cuda_graph = bool(e.get("cuda_graph", False)) and self._graph_ok(comm)
+            self._graph = None
+            self._graph_calls = 0
             # step N's AdamW runs on a side stream under step N+1's forward
-            if comm.get("overlap_optimizer", True) and not self._pipeline \
+            if comm.get("overlap_optimizer", True) and not self._pipeline and not self._cuda_graph \
                     and self.scaler is None and hasattr(self.optimizer, "enable_forward_overlap"):
                 self.optimizer.enable_forward_overlap(model)
             # single data rank: gradient sum-of-squares per bucket under backward
             # (opt-in: measured neutral on 6.7B, the GEMMs leave no CU slots free)
-            if comm.get("early_grad_norm", False) and not self._pipeline \
+            if comm.get("early_grad_norm", False) and not self._pipeline and not self._cuda_graph \
                     and hasattr(self.buffer, "enable_early_norm"):
                 self.buffer.enable_early_norm()
             # ZeRO-1/2: the post-update parameter all-gather hides under the next forward
@@ -244,7 +249,88 @@ class EagerEngine(BasicEngine):
                 logger.error("fault injection: rank %s exits at step %s" % (r, s))
                 os._exit(17)
 
+    # ------------------------------------------------------------------ HIP graph
+    def _graph_ok(self, comm):
+        """Whole-step capture needs a single-rank, non-pipelined bf16 step with
+        device-resident optimizer state (no host syncs, no loss scaler)."""
+        why = None
+        if not torch.cuda.is_available() or self.device.type != "cuda":
+            why = "no GPU"
+        elif self._distributed:
+            why = "multi-rank runs keep eager collectives"
+        elif self._pipeline:
+            why = "pipeline schedules run eagerly"
+        elif self._use_pure_fp16 and self._dtype == torch.float16:
+            why = "the fp16 loss scaler steps on the host"
+        elif getattr(self.optimizer, "offload", False):
+            why = "offloaded optimizer state"
+        if why is not None:
+            logger.warning("Engine.cuda_graph disabled: %s" % why)
+            return False
+        return True
+
+    def _graph_setup(self):
+        k = _lib.kernels()
+        self._graph_salt = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._graph_lr = torch.zeros(1, dtype=torch.float32, device=self.device)
+        k.set_dropout_salt(self._graph_salt.data_ptr())
+        k.set_adamw_lr_ptr(self._graph_lr.data_ptr())
+
+    def _graph_body(self, batch):
+        """The device work of one step: fresh dropout salt, forward, backward,
+        gradient finish, clip + AdamW, gradient reset."""
+        self._graph_salt.add_(1)
+        model = self._module.model
+        model.train()
+        micro = _split_micro(batch, self._accumulate_steps)
+        loss = None
+        for i, mb in enumerate(micro):
+            self.buffer.set_last_micro_batch(i == len(micro) - 1)
+            l = self._module.training_step(mb)
+            if self._accumulate_steps > 1:
+                l = l / self._accumulate_steps
+            self._module.backward(l)
+            loss = l.detach() if loss is None else loss + l.detach()
+        self.buffer.finish()
+        self.optimizer.step()
+        self.optimizer.clear_grad()
+        return loss
+
+    def _fit_graphed(self, batch, warmup=2):
+        """Capture the whole training step into one HIP graph after ``warmup``
+        eager steps (same kernels, same device-side salt / lr), then replay it.
+        Dropout draws new masks every replay (device salt); the learning rate
+        is written to the device before each replay; host bookkeeping
+        (scheduler, step counter) runs outside the graph."""
+        if self._graph_calls == 0:
+            self._graph_setup()
+        self._graph_calls += 1
+        self._graph_lr.fill_(float(self.optimizer.get_lr()))
+        if self._graph is None and self._graph_calls <= warmup:
+            loss = self._graph_body(batch)
+        elif self._graph is None:
+            torch.cuda.synchronize()
+            self._graph_static = [t.clone() if torch.is_tensor(t) else t for t in batch]
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._graph_loss = self._graph_body(self._graph_static)
+            self._graph = g
+            g.replay()  # the capture itself does not execute the step
+            loss = self._graph_loss
+        else:
+            for dst, src in zip(self._graph_static, batch):
+                if torch.is_tensor(dst):
+                    dst.copy_(src, non_blocking=True)
+            self._graph.replay()
+            self.optimizer.step_count += 1  # the captured step() ran its host part once
+            loss = self._graph_loss
+        if self.lr_scheduler is not None and hasattr(self.lr_scheduler, "step"):
+            self.lr_scheduler.step()
+        return loss
+
     def _fit_impl(self, batch):
+        if getattr(self, "_cuda_graph", False):
+            return self._fit_graphed(batch)
         model = self._module.model
         model.train()
         if self._pipeline:

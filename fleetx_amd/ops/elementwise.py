@@ -119,6 +119,7 @@ class _BiasDropoutAdd(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, bias, residual, p, key):
         ctx.p, ctx.key = p, key
+        ctx.bias = bias
         ctx.has_bias, ctx.has_res = bias is not None, residual is not None
         x = x.contiguous()
         cols = x.shape[-1]
@@ -154,8 +155,16 @@ class _BiasDropoutAdd(torch.autograd.Function):
                 part = torch.empty(splits, cols, device=dout.device, dtype=torch.float32)
                 k.dropout_bwd_colsum(dc, dout.data_ptr(), dx.data_ptr() if ctx.p > 0 else 0,
                                      part.data_ptr(), rows, cols, splits, float(ctx.p), ctx.key, st)
-                db = torch.empty(cols, device=dout.device, dtype=dout.dtype)
-                k.coltile_finalize(dc, part.data_ptr(), splits, cols, 0, db.data_ptr(), 0, st)
+                bias = ctx.bias
+                if bias is not None and getattr(bias, "_fx_fused_wgrad", False) \
+                        and hasattr(bias, "main_grad"):
+                    # fp32 bias gradient straight into main_grad
+                    from .norm import _into_main_grad
+                    _into_main_grad(bias, lambda mg, acc: k.coltile_finalize(
+                        dc, part.data_ptr(), splits, cols, mg.data_ptr(), 0, int(acc), st))
+                else:
+                    db = torch.empty(cols, device=dout.device, dtype=dout.dtype)
+                    k.coltile_finalize(dc, part.data_ptr(), splits, cols, 0, db.data_ptr(), 0, st)
             elif ctx.p > 0:
                 k.dropout_fwd(dc, dout.data_ptr(), dx.data_ptr(), dout.numel(), float(ctx.p),
                               ctx.key, st)

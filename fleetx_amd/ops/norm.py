@@ -29,6 +29,36 @@ def _col_reduce_ln(dy, s, mean, rstd, cols, dtype):
     return dg, db
 
 
+def _fused_param(p):
+    return p is not None and getattr(p, "_fx_fused_wgrad", False) and hasattr(p, "main_grad")
+
+
+def _into_main_grad(p, fill):
+    """Write (first contribution of the step) or accumulate a parameter's
+    gradient straight into its fp32 ``main_grad`` and report it ready."""
+    from ..parallel.linear import grad_part_done
+    fill(p.main_grad, not getattr(p, "_fx_fresh", False))
+    p._fx_fresh = False
+    grad_part_done(p)
+
+
+def _col_reduce_ln_main_grad(dy, s, mean, rstd, cols, dtype, weight, lnbias):
+    """LN weight/bias gradients reduced over rows straight into the fp32
+    ``main_grad`` of both parameters (no 16-bit grad, no autograd copy)."""
+    k = _lib.kernels()
+    rows = dy.numel() // cols
+    splits = k.coltile_splits(rows, cols)
+    p0 = torch.empty(splits, cols, device=dy.device, dtype=torch.float32)
+    p1 = torch.empty_like(p0)
+    st = _lib.stream()
+    dc = _lib.dt_code(dtype)
+    k.coltile_partial(dc, 0, dy.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                      p0.data_ptr(), p1.data_ptr(), rows, cols, splits, st)
+    for prm, part in ((weight, p0), (lnbias, p1)):
+        _into_main_grad(prm, lambda mg, acc, part=part: k.coltile_finalize(
+            dc, part.data_ptr(), splits, cols, mg.data_ptr(), 0, int(acc), st))
+
+
 def col_sum(x, cols):
     """Column sum of a [rows, cols] 16-bit tensor (fp32 accumulation)."""
     if not x.is_cuda:
@@ -111,6 +141,8 @@ class _AddLayerNorm(torch.autograd.Function):
             y = ((vf - mean.view(*vf.shape[:-1], 1)) * rstd.view(*vf.shape[:-1], 1) * weight.float()
                  + lnbias.float()).to(x.dtype)
         ctx.save_for_backward(s_saved, mean, rstd, weight)
+        # parameters whose gradients may go straight into main_grad
+        ctx.lnbias, ctx.bias = lnbias, bias
         ctx.return_sum = s is not None
         if s is None:
             return y
@@ -136,8 +168,17 @@ class _AddLayerNorm(torch.autograd.Function):
             k.ln_bwd_row(dc, dy.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                          weight.data_ptr(), _lib.ptr(ds_in), ds.data_ptr(), dx.data_ptr(), rows, h,
                          float(ctx.p), ctx.key, _lib.stream())
-            dw, db = _col_reduce_ln(dy, s, mean, rstd, h, dy.dtype)
-            dbias = col_sum(dx, h) if ctx.has_bias else None
+            if _fused_param(weight) and _fused_param(ctx.lnbias):
+                _col_reduce_ln_main_grad(dy, s, mean, rstd, h, dy.dtype, weight, ctx.lnbias)
+                dw = db = None
+            else:
+                dw, db = _col_reduce_ln(dy, s, mean, rstd, h, dy.dtype)
+            dbias = None
+            if ctx.has_bias:
+                if _fused_param(ctx.bias):
+                    _into_main_grad(ctx.bias, lambda mg, acc: col_sum_f32(dx, mg, acc))
+                else:
+                    dbias = col_sum(dx, h)
         else:
             sf = s.float().reshape(rows, h)
             xh = (sf - mean.view(rows, 1)) * rstd.view(rows, 1)
@@ -172,6 +213,9 @@ class FusedLayerNorm(torch.nn.Module):
         super().__init__()
         self.weight = torch.nn.Parameter(torch.ones(hidden, dtype=dtype, device=device))
         self.bias = torch.nn.Parameter(torch.zeros(hidden, dtype=dtype, device=device))
+        # backward reduces the LN gradients straight into the fp32 main_grad
+        self.weight._fx_fused_wgrad_ok = True
+        self.bias._fx_fused_wgrad_ok = True
         self.eps = eps
         self.normalized_shape = (hidden,)
 

@@ -150,6 +150,9 @@ class RowParallelLinear(nn.Module):
                                                           dtype=dtype, device=device,
                                                           init="zeros"))
             self.bias.sequence_parallel = self.sequence_parallel
+            # with skip_bias_add its gradient is reduced by the fused residual
+            # kernels straight into main_grad
+            self.bias._fx_fused_wgrad_ok = skip_bias_add
         else:
             self.register_parameter("bias", None)
 
