@@ -8,13 +8,12 @@
 // (tools/bench_gemm.py).  Transposing dy and x to token-contiguous copies
 // costs one read + one write of each at HBM speed, well under the GEMM saving.
 //
-// Tile: 64 x 64 elements per 256-thread workgroup (4 wave64s).  Loads are
-// 16-byte vectors along the source row (8 elements), two per thread; the tile
-// is staged in LDS with a 2-element row pad (row stride 33 dwords, so the
-// column gather of 8 consecutive rows hits 8 different banks), then each
-// thread gathers 8 source rows of one source column into one 16-byte store
-// along the destination row.  R, C, ldx, ldy are multiples of 8 (checked on
-// the host), so only whole 8-element chunks are ever bounds-checked.
+// Tile: 64 x 256 elements per 256-thread workgroup (4 wave64s).  Loads are
+// 16-byte vectors along the source row (8 elements), eight per thread; the
+// tile is staged in LDS with a 2-element row pad, then each thread gathers 8
+// source rows of one source column into one 16-byte store along the
+// destination row.  R, C, ldx, ldy are multiples of 8 (checked on the host),
+// so only whole 8-element chunks are ever bounds-checked.
 //
 // With ``part`` set the kernel also emits the fp32 column sums of its tile
 // (part[tile_row][col]) -- the bias gradient of the GEMM whose dy is being
@@ -24,33 +23,35 @@
 
 namespace {
 
-constexpr int TT = 64;
-constexpr int TPAD = 2;
+// Tile: 64 source rows x 256 source columns per 256-thread workgroup.  A
+// 64 x 64 tile reads 128-byte row pieces and measured 2.0-2.9 TB/s on the
+// transformer shapes; 512-byte row pieces and 8 loads in flight per thread
+// (16 KiB per wave) keep HBM streaming (tools/bench_gemm.py transpose_dy_hip).
+constexpr int TR = 64, TC = 256;
+constexpr int TPAD = 2;  // row stride 129 dwords: the 8-row column gathers spread over banks
 
 template <typename T, bool COLSUM>
 __global__ __launch_bounds__(256) void transpose16_kernel(const uint16_t* __restrict__ x,
                                                           uint16_t* __restrict__ y,
                                                           float* __restrict__ part, int R, int C,
                                                           long ldx, long ldy, int tiles_c) {
-  __shared__ uint16_t t[TT][TT + TPAD];
+  __shared__ uint16_t t[TR][TC + TPAD];
   const int bc = blockIdx.x % tiles_c;
   const int br = blockIdx.x / tiles_c;
-  const int r0 = br * TT, c0 = bc * TT;
+  const int r0 = br * TR, c0 = bc * TC;
   const int tid = threadIdx.x;
-  uint4 v[2];
+  uint4 v[8];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int id = tid + k * 256;
-    const int r = id >> 3, cc = (id & 7) * 8;
+  for (int k = 0; k < 8; ++k) {
+    const int r = (tid >> 5) + 8 * k, cc = (tid & 31) * 8;
     if (r0 + r < R && c0 + cc < C)
       v[k] = *reinterpret_cast<const uint4*>(x + (long)(r0 + r) * ldx + c0 + cc);
     else
       v[k] = make_uint4(0, 0, 0, 0);
   }
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int id = tid + k * 256;
-    const int r = id >> 3, cc = (id & 7) * 8;
+  for (int k = 0; k < 8; ++k) {
+    const int r = (tid >> 5) + 8 * k, cc = (tid & 31) * 8;
     uint32_t* d = reinterpret_cast<uint32_t*>(&t[r][cc]);
     d[0] = v[k].x;
     d[1] = v[k].y;
@@ -59,9 +60,9 @@ __global__ __launch_bounds__(256) void transpose16_kernel(const uint16_t* __rest
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < 8; ++k) {
     const int id = tid + k * 256;
-    const int c = id >> 3, rr = (id & 7) * 8;
+    const int c = id >> 3, rr = (id & 7) * 8;  // 8 lanes write one 128-byte output row piece
     uint16_t h[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) h[i] = t[rr + i][c];
@@ -87,8 +88,8 @@ extern "C" int fx_transpose16(int dtype, const void* x, void* y, float* part, in
                               long ldx, long ldy, hipStream_t st) {
   if ((R | C) & 7 || ldx & 7 || ldy & 7) return -1;
   if (R == 0 || C == 0) return 0;
-  const int tiles_c = (C + TT - 1) / TT;
-  const long blocks = (long)tiles_c * ((R + TT - 1) / TT);
+  const int tiles_c = (C + TC - 1) / TC;
+  const long blocks = (long)tiles_c * ((R + TR - 1) / TR);
   if (blocks > 0x7fffffffL) return -2;
   const uint16_t* xs = reinterpret_cast<const uint16_t*>(x);
   uint16_t* ys = reinterpret_cast<uint16_t*>(y);

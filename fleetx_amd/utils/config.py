@@ -193,6 +193,7 @@ def _fill_defaults(config):
     comm.setdefault("tp_row_chunks", 2)
     comm.setdefault("sp_chunks", 2)             # SP all-gather / reduce-scatter chunks
     eng = config.setdefault("Engine", AttrDict())
+    eng.setdefault("cuda_graph", False)        # whole-step HIP graph (single rank)
     mp = eng.setdefault("mix_precision", AttrDict())
     mp.setdefault("use_pure_fp16", False)
     mp.setdefault("dtype", "bfloat16")
