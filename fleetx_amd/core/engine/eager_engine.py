@@ -207,6 +207,13 @@ class EagerEngine(BasicEngine):
                     decr_every=int(amp.get("decr_every_n_nan_or_inf", 2)),
                     device=self.device)
                 self.optimizer.loss_scale = self.scaler.scale
+            # weight-gradient GEMMs beside the data-gradient chain (parallel/linear.py)
+            ws = comm.get("wgrad_stream", "auto")
+            if ws == "auto":
+                ws = configs.Model.get("hidden_size", 0) <= 2048
+            from ...parallel import linear as _lin
+            _lin.WGRAD_STREAM["enabled"] = bool(ws) and self.device.type == "cuda" \
+                and type(self.buffer) is FlatParamGradBuffer
             # whole-step HIP graph (Engine.cuda_graph): one replay per step
             self._cuda_graph = bool(e.get("cuda_graph", False)) and self._graph_ok(comm)
             self._graph = None

@@ -285,6 +285,8 @@ class FlatParamGradBuffer:
         if b.launched:
             return
         b.launched = True
+        from .linear import join_wgrad_stream
+        join_wgrad_stream()  # weight gradients computed on the side stream are final
         seg = self.grad_flat[b.start:b.end]
         works = []
         if self._norm_stream is not None:  # _launch only runs on final gradients
@@ -318,6 +320,8 @@ class FlatParamGradBuffer:
 
     def finish(self):
         """Complete every gradient collective; average over the data world."""
+        from .linear import join_wgrad_stream
+        join_wgrad_stream()
         for n, p in self.params:
             if p._fx_fresh:  # no gradient this step
                 p.main_grad.zero_()

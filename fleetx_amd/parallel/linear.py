@@ -79,6 +79,31 @@ def _tn_operands(dy2, x2, colsum=None):
     return transpose2d(dy2, colsum=colsum), transpose2d(x2).t()
 
 
+# Weight-gradient GEMMs on a side stream (Distributed.comm.wgrad_stream): the
+# data-gradient chain of backward never waits for them, so on models whose
+# GEMMs under-fill the 256 CUs (hidden <= 2048: 8192 x 1024 x 1024 is 128
+# tiles of 256 x 256) the wgrad of layer l runs beside the dgrad of layer l-1.
+# Joined by the gradient buffer before any collective / the optimizer.
+WGRAD_STREAM = {"enabled": False, "stream": None}
+
+
+def _wgrad_side_stream(dev):
+    if not WGRAD_STREAM["enabled"]:
+        return None
+    s = WGRAD_STREAM["stream"]
+    if s is None or s.device != dev:
+        s = torch.cuda.Stream(device=dev)
+        WGRAD_STREAM["stream"] = s
+    return s
+
+
+def join_wgrad_stream():
+    """Order the current stream after every weight gradient issued so far."""
+    s = WGRAD_STREAM["stream"]
+    if s is not None and WGRAD_STREAM["enabled"]:
+        torch.cuda.current_stream(s.device).wait_stream(s)
+
+
 def accumulate_wgrad(weight, dy2, x2, bias=None, notify=True):
     """``weight.main_grad (+)= dy2^T @ x2`` in fp32; notifies the grad buffer
     (``notify=False``: a partial contribution, more follow in this backward).
@@ -86,6 +111,24 @@ def accumulate_wgrad(weight, dy2, x2, bias=None, notify=True):
     With ``bias`` (a Parameter) the bias gradient ``sum_rows(dy2)`` is produced
     too: straight into ``bias.main_grad`` when the bias takes fused grads
     (returns None), else returned as a tensor for autograd."""
+    side = _wgrad_side_stream(dy2.device) if dy2.is_cuda and (bias is None or _fused(bias)) \
+        else None
+    if side is None:
+        return _accumulate_wgrad(weight, dy2, x2, bias, notify)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        _accumulate_wgrad(weight, dy2, x2, bias, notify=False, bias_notify=False)
+    dy2.record_stream(side)
+    x2.record_stream(side)
+    # readiness callbacks may launch collectives: those join the side stream
+    if bias is not None:
+        grad_part_done(bias)
+    if notify:
+        grad_part_done(weight)
+    return None
+
+
+def _accumulate_wgrad(weight, dy2, x2, bias=None, notify=True, bias_notify=True):
     mg = weight.main_grad
     fresh = getattr(weight, "_fx_fresh", False)
     if G.use("wgrad", dy2, x2) and G.linear_wgrad(dy2, x2, mg, not fresh):
@@ -94,7 +137,8 @@ def accumulate_wgrad(weight, dy2, x2, bias=None, notify=True):
             if _fused(bias):
                 colsum_into(dy2, bias.main_grad, not getattr(bias, "_fx_fresh", False))
                 bias._fx_fresh = False
-                grad_part_done(bias)
+                if bias_notify:
+                    grad_part_done(bias)
             else:
                 db = torch.empty(bias.shape, device=dy2.device, dtype=torch.float32)
                 colsum_into(dy2, db, False)
@@ -120,7 +164,8 @@ def accumulate_wgrad(weight, dy2, x2, bias=None, notify=True):
     if bias is not None:
         if db is None:
             bias._fx_fresh = False
-            grad_part_done(bias)
+            if bias_notify:
+                grad_part_done(bias)
         else:
             db = db.to(bias.dtype)
     a, b = tn if tn is not None else (dy2.t(), x2)

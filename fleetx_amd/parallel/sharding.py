@@ -383,6 +383,8 @@ class Stage3ParamGradBuffer:
                 u.full_grad[prev:seg.fend].zero_()
 
     def _launch_rs(self, u):
+        from .linear import join_wgrad_stream
+        join_wgrad_stream()
         self._zero_missing(u)
         works, pieces = [], []
         for seg in u.segments:
@@ -443,6 +445,8 @@ class Stage3ParamGradBuffer:
 
     def finish(self):
         """Complete every reduction; average over the data world."""
+        from .linear import join_wgrad_stream
+        join_wgrad_stream()
         for u in self.units:
             if u.grad_live and not u.done:  # backward never reached every param
                 self._launch_rs(u)

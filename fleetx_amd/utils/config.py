@@ -192,6 +192,7 @@ def _fill_defaults(config):
     comm.setdefault("tp_overlap", True)         # async dX all-reduce / chunked row all-reduce
     comm.setdefault("tp_row_chunks", 2)
     comm.setdefault("sp_chunks", 2)             # SP all-gather / reduce-scatter chunks
+    comm.setdefault("wgrad_stream", "auto")     # wgrad GEMMs on a side stream (auto: hidden<=2048)
     eng = config.setdefault("Engine", AttrDict())
     eng.setdefault("cuda_graph", False)        # whole-step HIP graph (single rank)
     mp = eng.setdefault("mix_precision", AttrDict())
