@@ -278,7 +278,8 @@ class EagerEngine(BasicEngine):
 
     def _graph_setup(self):
         k = _lib.kernels()
-        self._graph_salt = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._graph_salt = torch.full((1,), getattr(self, "_graph_salt_resume", 0),
+                                      dtype=torch.int64, device=self.device)
         self._graph_lr = torch.zeros(1, dtype=torch.float32, device=self.device)
         k.set_dropout_salt(self._graph_salt.data_ptr())
         k.set_adamw_lr_ptr(self._graph_lr.data_ptr())
@@ -583,6 +584,9 @@ class EagerEngine(BasicEngine):
                 "rng_tracker": get_rng_state_tracker().get_states()}
         if self.scaler is not None:
             meta["scaler"] = self.scaler.state_dict()
+        if getattr(self, "_graph_salt", None) is not None:
+            # graph mode: the device dropout salt continues after a resume
+            meta["graph_salt"] = int(self._graph_salt.item())
         if torch.cuda.is_available():
             meta["cuda_rng_state"] = torch.cuda.get_rng_state()
         payloads["meta_state.pdopt"] = meta
@@ -631,6 +635,9 @@ class EagerEngine(BasicEngine):
             self.consumed_samples = int(meta.get("consumed_samples", 0))
             if "rng_tracker" in meta:
                 get_rng_state_tracker().set_states(meta["rng_tracker"])
+            self._graph_salt_resume = int(meta.get("graph_salt", 0))
+            if getattr(self, "_graph_salt", None) is not None:
+                self._graph_salt.fill_(self._graph_salt_resume)
             if self.scaler is not None and "scaler" in meta:
                 self.scaler.load_state_dict(meta["scaler"])
             if "cuda_rng_state" in meta and torch.cuda.is_available():

@@ -81,3 +81,22 @@ def test_graph_dropout_masks_change_per_replay():
     from fleetx_amd.ops import _lib
     _lib.kernels().set_dropout_salt(0)
     _lib.kernels().set_adamw_lr_ptr(0)
+
+
+def test_graph_salt_checkpointed(tmp_path):
+    """The device dropout salt is saved and restored, so a resumed graph-mode
+    run continues the mask sequence instead of replaying it."""
+    eng = _engine(True, 0.1)
+    _run(eng, _batches(4))
+    eng._output_dir = str(tmp_path)
+    eng.save(epoch=0, step=4)
+    salt = int(eng._graph_salt.item())
+    assert salt == 4
+    eng2 = _engine(True, 0.1)
+    import glob
+    eng2.load(ckpt_dir=glob.glob(str(tmp_path / "epoch_0_step_4*"))[0])
+    _run(eng2, _batches(1))
+    assert int(eng2._graph_salt.item()) == salt + 1
+    from fleetx_amd.ops import _lib
+    _lib.kernels().set_dropout_salt(0)
+    _lib.kernels().set_adamw_lr_ptr(0)
