@@ -49,6 +49,7 @@ def set_mode(mode):
 # Measured on the 6.7B step (profiles/r2_gemm/): every kind currently costs
 # 8-17 ms/step against hipBLASLt, so none is routed by default.
 AUTO_KINDS = set(k for k in os.environ.get("FLEETX_GEMM_AUTO", "").split(",") if k)
+_AUTO_WGRAD = os.environ.get("FLEETX_GEMM_AUTO_WGRAD", "1") == "1"  # shape-routed wgrad
 
 
 def use(kind, a, b=None):
@@ -58,7 +59,21 @@ def use(kind, a, b=None):
     if _MODE == "blas" or not a.is_cuda or a.dtype not in (torch.bfloat16, torch.float16):
         return False
     if _MODE == "auto":
-        return kind in AUTO_KINDS
+        if kind in AUTO_KINDS:
+            return True
+        if kind == "wgrad" and _AUTO_WGRAD and b is not None:
+            # measured routing (tools/bench_gemm.py, profiles/r2_final/gemm_hidden_sweep.jsonl):
+            # the fp32-accumulating weight-gradient GEMM in the native token-major
+            # layout beats hipBLASLt's TN path plus its two transposes when the
+            # [N, K] output is one to two waves of 256x256 tiles on the 256 CUs
+            # (1.3B QKV/FC1/FC2 +3/+15/+11 % isolated, +0.7 % on the whole 1.3B step);
+            # more tiles favour hipBLASLt, fewer leave CUs idle.  The 6.7B
+            # out-proj (4096 x 4096, +7 % isolated) measured -0.3 % in the step,
+            # so square 4096+ outputs stay on hipBLASLt
+            N, K = a.shape[1], b.shape[1]
+            tiles = (N // 256) * (K // 256)
+            return 192 <= tiles <= 512 and min(N, K) <= 2048
+        return False
     return True
 
 
