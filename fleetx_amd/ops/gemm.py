@@ -70,11 +70,15 @@ def use(kind, a, b=None):
             # more tiles favour hipBLASLt, fewer leave CUs idle.  The 6.7B
             # out-proj (4096 x 4096, +7 % isolated) measured -0.3 % in the step,
             # so square 4096+ outputs stay on hipBLASLt
-            N, K = a.shape[1], b.shape[1]
-            tiles = (N // 256) * (K // 256)
-            return 192 <= tiles <= 512 and min(N, K) <= 2048
+            return wgrad_routed(a.shape[1], b.shape[1])
         return False
     return True
+
+
+def wgrad_routed(N, K):
+    """Whether the auto routing sends a ``[N, K]`` weight gradient to the MFMA kernel."""
+    tiles = (N // 256) * (K // 256)
+    return 192 <= tiles <= 512 and min(N, K) <= 2048
 
 
 def _ok(*ts):

@@ -1,0 +1,43 @@
+"""CPU-side logic of the round-2 runtime pieces: the communicator's RCCL/gloo
+fallback (no one-shot kernel off the GPU), the measured GEMM routing table,
+and the decode-split rule."""
+import torch
+import torch.distributed as dist
+
+from tests import dist_utils
+
+
+def _comm_worker(rank, world):
+    from fleetx_amd.parallel.comm import Communicator
+    from fleetx_amd.parallel.topology import CommGroup
+    g = CommGroup(list(range(world)), None)
+    c = Communicator(g)
+    assert c.oneshot is None  # gloo / CPU: plain torch.distributed
+    x = torch.full((5,), float(rank + 1))
+    y = c.all_reduce(x.clone())
+    m = c.all_reduce(torch.tensor([float(rank)]), dist.ReduceOp.MAX)
+    return y.tolist(), m.item()
+
+
+def test_communicator_falls_back_to_torch_distributed():
+    res = dist_utils.run(_comm_worker, 2)
+    for y, m in res:
+        assert y == [3.0] * 5 and m == 1.0
+
+
+def test_wgrad_routing_table():
+    from fleetx_amd.ops.gemm import wgrad_routed
+    # 1.3B: QKV (6144 x 2048), FC1 (8192 x 2048), FC2 (2048 x 8192) -> MFMA kernel
+    assert wgrad_routed(6144, 2048) and wgrad_routed(8192, 2048) and wgrad_routed(2048, 8192)
+    # 1.3B out-proj (too few tiles), 6.7B shapes, 345M shapes, LM head -> hipBLASLt
+    assert not wgrad_routed(2048, 2048)
+    assert not wgrad_routed(4096, 4096) and not wgrad_routed(16384, 4096)
+    assert not wgrad_routed(1024, 1024) and not wgrad_routed(4096, 1024)
+    assert not wgrad_routed(50304, 2048)
+
+
+def test_decode_split_rule():
+    from fleetx_amd.ops.attention import decode_splits
+    assert decode_splits(1, 16, 192) == 1          # short context: one split, no combine
+    assert decode_splits(1, 32, 32768) == 64       # long context fills the chip
+    assert decode_splits(64, 32, 32768) == 1       # enough (b, h) pairs already
