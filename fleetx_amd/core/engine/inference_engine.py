@@ -9,7 +9,11 @@ MI355X design: the network is rebuilt from the export directory on the HIP
 kernels (bf16 on GPU) and, for a fixed input shape, its forward is captured
 once into a HIP graph (``torch.cuda.CUDAGraph`` is hipGraph on ROCm) and
 replayed -- the "static graph" of the reference without a tracing compiler.
-Generation modules run their KV-cache decode loop eagerly.
+Generation modules run their KV-cache decode loop with the per-token step
+replayed from a HIP graph and each decoder layer as five fused kernels
+(``gpt/generation.py``: weight-streaming GEMVs with QKV/KV-cache, GeLU and
+residual epilogues -- the fused_multi_transformer counterpart); mp > 1 decode
+all-reduces take the one-shot IPC kernel (``parallel/comm.py``).
 """
 import os
 
