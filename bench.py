@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--sequence-parallel", action="store_true")
     ap.add_argument("--no-dropout", action="store_true")
+    ap.add_argument("--grad-reduce-dtype", default=None, choices=["float32", "bfloat16"],
+                    help="gradient reduction wire dtype (default: bf16 when N > 1)")
     ap.add_argument("--hip-graph", type=int, default=-1,
                     help="capture the whole step in one HIP graph (1/0; default: on for "
                          "the 345M-class model on one GPU, where launches show; 1.3B+ keep the "
@@ -119,6 +121,10 @@ def main():
           "Engine.save_load.save_steps=-1", "Engine.mix_precision.dtype=bfloat16",
           "Data.Train.dataset.max_seq_len=%d" % args.seq,
           "Data.Train.dataset.name=SyntheticGPTDataset"]
+    # multi-GPU: gradients cross xGMI as bf16 (fp32 accumulation in the owner),
+    # as the reference's fp16 O2 gradients do -- half the reduce-scatter bytes
+    grad_wire = args.grad_reduce_dtype or ("bfloat16" if n > 1 else "float32")
+    ov.append("Distributed.comm.reduce_dtype=%s" % grad_wire)
     graph = args.hip_graph if args.hip_graph >= 0 else int(n == 1 and h <= 1024)
     ov.append("Engine.cuda_graph=%s" % bool(graph))
     # A/B experiments: extra config overrides, e.g. "Distributed.comm.early_grad_norm=False"
@@ -187,6 +193,7 @@ def main():
             "config": {"model": args.model, "global_batch": global_batch, "seq_len": S,
                        "parallelism": par, "micro_batch": micro,
                        "hip_graph": bool(getattr(engine, "_cuda_graph", False)),
+                       "grad_reduce_dtype": grad_wire,
                        "dropout": drop, "recompute": recompute},
             "mfu": round(mfu, 4), "tokens_per_gpu": round(tps / n, 1),
             "final_loss": round(lval, 4),
