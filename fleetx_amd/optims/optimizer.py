@@ -15,6 +15,7 @@ the clip coefficient and the fp16 found-inf flag stay on the device, so a
 step never synchronises the host.
 """
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -157,6 +158,7 @@ class FlatOptimizer:
 
     # ------------------------------------------------------------------ overlap
     _overlap_groups = None
+    overlap_grid = 128  # Distributed.comm.overlap_optimizer_grid
 
     def enable_forward_overlap(self, model):
         """Run the parameter update of step N on a side stream, unit by unit
@@ -277,6 +279,14 @@ class FusedAdamW(FlatOptimizer):
         dt = _lib.dt_code(pf.dtype)
         os_ = self._opt_stream
         os_.wait_stream(torch.cuda.current_stream())  # grads final, clip scale computed
+        # Cap the overlapped update's workgroups: uncapped it fills every CU and
+        # the forward GEMMs queue behind it (the overlap then buys nothing);
+        # with 128 workgroups it streams at ~2 TB/s beside the GEMMs and ends
+        # with the forward (6.7B step -1.5..-1.8 % on two boxes,
+        # profiles/r2_final/adamw_overlap_grid.txt).  0 = uncapped.
+        grid = int(os.environ.get("FLEETX_ADAMW_OVERLAP_GRID", str(self.overlap_grid)))
+        if grid:
+            k.adamw_tune(grid, 1)
         with torch.cuda.stream(os_):
             st = _lib.stream()
             for u, pieces in self._overlap_groups:
@@ -292,6 +302,8 @@ class FusedAdamW(FlatOptimizer):
                 ev = torch.cuda.Event()
                 ev.record(os_)
                 self._unit_events[u] = ev
+        if grid:
+            k.adamw_tune(0, 1)
 
     def _update_offloaded(self, lr):
         """Stream host-resident master/m/v through the GPU in chunks: the H2D
