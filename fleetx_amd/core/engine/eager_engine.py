@@ -305,6 +305,16 @@ class EagerEngine(BasicEngine):
         self.optimizer.clear_grad()
         return loss
 
+    def _graph_batch_matches(self, batch):
+        if len(batch) != len(self._graph_static):
+            return False
+        for a, b in zip(self._graph_static, batch):
+            if torch.is_tensor(a) != torch.is_tensor(b):
+                return False
+            if torch.is_tensor(a) and (a.shape != b.shape or a.dtype != b.dtype):
+                return False
+        return True
+
     def _fit_graphed(self, batch, warmup=2):
         """Capture the whole training step into one HIP graph after ``warmup``
         eager steps (same kernels, same device-side salt / lr), then replay it.
@@ -326,6 +336,10 @@ class EagerEngine(BasicEngine):
             self._graph = g
             g.replay()  # the capture itself does not execute the step
             loss = self._graph_loss
+        elif not self._graph_batch_matches(batch):
+            # a batch of another shape (e.g. a short last batch): run it eagerly
+            # with the same device-side salt / lr; the graph stays for the rest
+            loss = self._graph_body(batch)
         else:
             for dst, src in zip(self._graph_static, batch):
                 if torch.is_tensor(dst):

@@ -100,3 +100,20 @@ def test_graph_salt_checkpointed(tmp_path):
     from fleetx_amd.ops import _lib
     _lib.kernels().set_dropout_salt(0)
     _lib.kernels().set_adamw_lr_ptr(0)
+
+
+def test_graph_short_batch_runs_eagerly():
+    """A batch of another shape than the captured one runs eagerly (and the
+    graph keeps serving the regular batches)."""
+    eng = _engine(True, 0.0)
+    bs = _batches(4)
+    _run(eng, bs[:3])
+    assert eng._graph is not None
+    short = [t[:2].contiguous() for t in bs[3]]
+    l_short = float(eng._fit_impl(short))
+    l_next = float(eng._fit_impl(bs[0]))
+    assert l_short == l_short and l_next == l_next
+    assert eng.optimizer.step_count == 5 and int(eng.optimizer.dev_step.item()) == 5
+    from fleetx_amd.ops import _lib
+    _lib.kernels().set_dropout_salt(0)
+    _lib.kernels().set_adamw_lr_ptr(0)
