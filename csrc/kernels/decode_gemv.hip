@@ -39,7 +39,6 @@
 namespace {
 
 enum { GV_BIAS = 0, GV_GELU = 1, GV_RES = 2, GV_QKV = 3 };
-constexpr int GV_KS = 4;  // waves per block, each on its own K range
 
 struct GemvArgs {
   const uint16_t* x;
@@ -93,7 +92,7 @@ __device__ __forceinline__ void mma_batch(floatx4& acc, const short8 (&wv)[U][2]
   }
 }
 
-template <typename T, int EPI, int U>
+template <typename T, int EPI, int U, int GV_KS>
 __global__ __launch_bounds__(64 * GV_KS) void gemv_kernel(GemvArgs a) {
   __shared__ float red[GV_KS * 256];
   const int lane = threadIdx.x & 63;
@@ -123,6 +122,7 @@ __global__ __launch_bounds__(64 * GV_KS) void gemv_kernel(GemvArgs a) {
   for (int j = 0; j < 4; ++j) red[w * 256 + (4 * g + j) * 16 + r] = acc[j];
   __syncthreads();
   const int t = threadIdx.x;  // (nn, m) = (t / 16, t % 16)
+  if (t >= 256) return;
   const int nn = t >> 4, m = t & 15;
   const int n = n0 + nn;
   if (m >= a.M || n >= a.N) return;
@@ -149,10 +149,15 @@ __global__ __launch_bounds__(64 * GV_KS) void gemv_kernel(GemvArgs a) {
 }
 
 template <typename T, int EPI>
-void launch_u(const GemvArgs& a, int u, hipStream_t s) {
+void launch_u(const GemvArgs& a, int u, int ks, hipStream_t s) {
   const dim3 grid((a.N + 15) / 16);
-  if (u >= 8) hipLaunchKernelGGL((gemv_kernel<T, EPI, 8>), grid, dim3(64 * GV_KS), 0, s, a);
-  else hipLaunchKernelGGL((gemv_kernel<T, EPI, 4>), grid, dim3(64 * GV_KS), 0, s, a);
+  if (ks == 8) {
+    if (u >= 8) hipLaunchKernelGGL((gemv_kernel<T, EPI, 8, 8>), grid, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((gemv_kernel<T, EPI, 4, 8>), grid, dim3(512), 0, s, a);
+  } else {
+    if (u >= 8) hipLaunchKernelGGL((gemv_kernel<T, EPI, 8, 4>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((gemv_kernel<T, EPI, 4, 4>), grid, dim3(256), 0, s, a);
+  }
 }
 
 }  // namespace
@@ -165,7 +170,11 @@ int fx_decode_gemv(int dt, int epi, int M, int N, int K, const void* x, long ldx
                    long ldw, const void* bias, const void* res, long ldres, void* y, long ldy,
                    void* kc, void* vc, const long* pos, int heads, int head_dim, int maxlen,
                    hipStream_t s) {
-  if (M < 1 || M > 16 || K % (64 * GV_KS * 4) != 0 || (ldx % 8) || (ldw % 8)) return 0;
+  if (M < 1 || M > 16 || K % 1024 != 0 || (ldx % 8) || (ldw % 8)) return 0;
+  // many column tiles: 8 waves per block, each on a shorter K range (more
+  // waves resident, shorter dependent chains); few tiles: 4 waves with two
+  // batches of loads in flight each (tools/bench_gemv.py)
+  const int ks = (N >= 8192 && K % 2048 == 0) ? 8 : 4;
   GemvArgs a;
   a.x = (const uint16_t*)x; a.w = (const uint16_t*)w; a.bias = (const uint16_t*)bias;
   a.res = (const uint16_t*)res; a.y = (uint16_t*)y;
@@ -173,13 +182,13 @@ int fx_decode_gemv(int dt, int epi, int M, int N, int K, const void* x, long ldx
   a.M = M; a.N = N; a.K = K;
   a.kc = (uint16_t*)kc; a.vc = (uint16_t*)vc; a.pos = pos;
   a.heads = heads; a.head_dim = head_dim; a.maxlen = maxlen;
-  const int u = (K / (64 * GV_KS)) % 8 == 0 ? 8 : 4;
+  const int u = (K / (64 * ks)) % 8 == 0 && K / (64 * ks) >= 16 ? 8 : 4;
 #define FX_GV(T)                                                  \
   switch (epi) {                                                  \
-    case GV_GELU: launch_u<T, GV_GELU>(a, u, s); break;           \
-    case GV_RES: launch_u<T, GV_RES>(a, u, s); break;             \
-    case GV_QKV: launch_u<T, GV_QKV>(a, u, s); break;             \
-    default: launch_u<T, GV_BIAS>(a, u, s); break;                \
+    case GV_GELU: launch_u<T, GV_GELU>(a, u, ks, s); break;           \
+    case GV_RES: launch_u<T, GV_RES>(a, u, ks, s); break;             \
+    case GV_QKV: launch_u<T, GV_QKV>(a, u, ks, s); break;             \
+    default: launch_u<T, GV_BIAS>(a, u, ks, s); break;                \
   }
   if (dt == 0) { FX_GV(bf16) } else { FX_GV(f16) }
 #undef FX_GV
