@@ -32,6 +32,10 @@ MODELS = {
     "gpt3-1.3B": (2048, 24, 16),
     "gpt-345M": (1024, 24, 16),
     "gpt-tiny": (256, 2, 4),
+    # GPT-3 175B layer shapes (h 12288, 96 heads) with 4 layers: the kernels of
+    # BASELINE config 4 measured on one GPU (the full model needs 16 nodes:
+    # configs/nlp/gpt/pretrain_gpt_175B_tp8_sharding16_stage3.yaml)
+    "gpt3-175B-4L": (12288, 4, 96),
 }
 from fleetx_amd.utils.hw import PEAK_DENSE_FLOPS  # noqa: E402
 PEAK_BF16 = PEAK_DENSE_FLOPS["bfloat16"]  # MI355X dense bf16 (spec), per GPU

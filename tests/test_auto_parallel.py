@@ -167,3 +167,21 @@ def test_semi_auto_wrong_annotation_refused():
     res = run(_lowering_worker, 2, 2, 1, True)
     for r in res:
         assert r["refused"] and "fc1" in r["refused"], r
+
+
+def test_175B_tp8_zero3_recipe_fits_hbm():
+    """BASELINE config 4: the 175B shape with TP8 + ZeRO-3 (+ recompute) is
+    sized for 288 GB per GPU on 16 nodes; one node alone cannot hold it."""
+    from fleetx_amd.utils import config as C
+    cfg = C.get_config(os.path.join(ROOT, "fleetx_amd/configs/nlp/gpt/"
+                                    "pretrain_gpt_175B_tp8_sharding16_stage3.yaml"), nranks=128)
+    d, m = cfg.Distributed, cfg.Model
+    assert d.mp_degree * d.sharding.sharding_degree * d.dp_degree * d.pp_degree == 128
+    est = P.estimate(m.hidden_size, m.num_layers, m.num_attention_heads, m.vocab_size,
+                     m.max_position_embeddings, cfg.Global.global_batch_size, d.dp_degree,
+                     d.mp_degree, d.pp_degree, d.sharding.sharding_degree,
+                     d.sharding.sharding_stage, cfg.Global.micro_batch_size, True)
+    assert est is not None and est[1] < P.HBM_BYTES * P.USABLE
+    assert est[1] < 60e9  # stage 3 keeps ~1/128 of the states per GPU
+    with pytest.raises(ValueError):
+        P.plan(12288, 96, 96, 51200, 2048, 8, 8)
