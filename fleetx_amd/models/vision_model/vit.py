@@ -23,12 +23,30 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ... import ops
+from ...parallel.linear import fused_mlp, linear
 
 
 def _xavier(lin):
     nn.init.xavier_uniform_(lin.weight)
     if lin.bias is not None:
         nn.init.zeros_(lin.bias)
+    return lin
+
+
+def _apply(mod, x, bias=True):
+    """A linear layer: the fused-gradient GEMM for a plain ``nn.Linear``, the
+    module itself otherwise (e.g. a QAT-wrapped layer, utils/qat.py)."""
+    if type(mod) is nn.Linear:
+        return linear(x, mod.weight, mod.bias if bias else None)
+    return mod(x)
+
+
+def _fused_grads(lin):
+    """Let the linear's weight / bias gradients go straight into the flat fp32
+    ``main_grad`` buffer (parallel/linear.py, ops/norm.py)."""
+    lin.weight._fx_fused_wgrad_ok = True
+    if lin.bias is not None:
+        lin.bias._fx_fused_wgrad_ok = True
     return lin
 
 
@@ -75,31 +93,41 @@ class Attention(nn.Module):
         self.num_heads = num_heads
         self.head_dim = dim // num_heads
         self.scale = qk_scale or self.head_dim ** -0.5
-        self.qkv = _xavier(nn.Linear(dim, dim * 3, bias=qkv_bias))
-        self.proj = _xavier(nn.Linear(dim, dim))
+        self.qkv = _fused_grads(_xavier(nn.Linear(dim, dim * 3, bias=qkv_bias)))
+        self.proj = _fused_grads(_xavier(nn.Linear(dim, dim)))
         self.attn_drop = attn_drop
         self.proj_drop = nn.Dropout(proj_drop)
 
-    def forward(self, x):
+    def _core(self, x):
         B, N, C = x.shape
-        qkv = self.qkv(x).view(B, N, 3, self.num_heads, self.head_dim)
+        qkv = _apply(self.qkv, x).view(B, N, 3, self.num_heads, self.head_dim)
         q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
         p = self.attn_drop if self.training else 0.0
         key = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
         o = ops.flash_attention(q, k, v, causal=False, dropout_p=p, key=key, scale=self.scale)
-        return self.proj_drop(self.proj(o.reshape(B, N, C)))
+        return o.reshape(B, N, C)
+
+    def forward_nobias(self, x):
+        """(proj(o) without its bias, bias): the bias joins the fused residual
+        + LayerNorm kernel of the block."""
+        return linear(self._core(x), self.proj.weight), self.proj.bias
+
+    def forward(self, x):
+        return self.proj_drop(_apply(self.proj, self._core(x)))
 
 
 class Mlp(nn.Module):
     def __init__(self, dim, hidden, drop=0.0):
         super().__init__()
-        self.fc1 = _xavier(nn.Linear(dim, hidden))
-        self.fc2 = _xavier(nn.Linear(hidden, dim))
+        self.fc1 = _fused_grads(_xavier(nn.Linear(dim, hidden)))
+        self.fc2 = _fused_grads(_xavier(nn.Linear(hidden, dim)))
         self.drop = nn.Dropout(drop)
 
     def forward(self, x):
-        h = ops.bias_gelu(F.linear(x, self.fc1.weight), self.fc1.bias, approximate=False)
-        return self.drop(self.fc2(self.drop(h)))
+        if type(self.fc1) is not nn.Linear:
+            return self.drop(self.fc2(self.drop(F.gelu(self.fc1(x)))))
+        h = ops.bias_gelu(linear(x, self.fc1.weight), self.fc1.bias, approximate=False)
+        return self.drop(_apply(self.fc2, self.drop(h)))
 
 
 class Block(nn.Module):
@@ -112,7 +140,23 @@ class Block(nn.Module):
         self.norm2 = ops.FusedLayerNorm(dim, epsilon)
         self.mlp = Mlp(dim, int(dim * mlp_ratio), drop)
 
+    def _fusable(self):
+        plain = all(type(m) is nn.Linear for m in (self.attn.qkv, self.attn.proj, self.mlp.fc1,
+                                                    self.mlp.fc2))
+        return plain and (self.drop_path.p == 0.0 or not self.training) and \
+            (self.attn.proj_drop.p == 0.0 and self.mlp.drop.p == 0.0 or not self.training)
+
     def forward(self, x):
+        if self._fusable():
+            # residual + proj bias + LN2 in one kernel, FFN1+GeLU(erf)+FFN2 as one
+            # autograd node, residual + FFN2 bias in one kernel; every weight and
+            # bias gradient lands in fp32 main_grad (same blocks as the GPT layer)
+            a, ab = self.attn.forward_nobias(self.norm1(x))
+            x2, h2 = ops.add_layer_norm(a, ab, x, self.norm2.weight, self.norm2.bias,
+                                        self.norm2.eps)
+            m = fused_mlp(h2, self.mlp.fc1.weight, self.mlp.fc1.bias, self.mlp.fc2.weight,
+                          act="gelu_erf")
+            return ops.bias_dropout_add(m, self.mlp.fc2.bias, x2)
         x = x + self.drop_path(self.attn(self.norm1(x)))
         return x + self.drop_path(self.mlp(self.norm2(x)))
 

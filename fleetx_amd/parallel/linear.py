@@ -79,11 +79,14 @@ def _tn_operands(dy2, x2, colsum=None):
     return transpose2d(dy2, colsum=colsum), transpose2d(x2).t()
 
 
-# Weight-gradient GEMMs on a side stream (Distributed.comm.wgrad_stream): the
-# data-gradient chain of backward never waits for them, so on models whose
+# Weight-gradient GEMMs on a side stream (Distributed.comm.wgrad_stream, opt-in):
+# the data-gradient chain of backward never waits for them, so on models whose
 # GEMMs under-fill the 256 CUs (hidden <= 2048: 8192 x 1024 x 1024 is 128
-# tiles of 256 x 256) the wgrad of layer l runs beside the dgrad of layer l-1.
-# Joined by the gradient buffer before any collective / the optimizer.
+# tiles of 256 x 256) the wgrad of layer l runs beside the dgrad of layer l-1
+# (+1.5 % on 345M / 1.3B).  Joined by the gradient buffer before any collective
+# / the optimizer.  Off by default: two concurrent library GEMMs can both be
+# stream-K kernels whose resident workgroups spin on tiles the other kernel's
+# workgroups keep from being scheduled -- a GPU deadlock, observed on ViT-g.
 WGRAD_STREAM = {"enabled": False, "stream": None}
 
 

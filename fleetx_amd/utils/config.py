@@ -192,7 +192,7 @@ def _fill_defaults(config):
     comm.setdefault("tp_overlap", True)         # async dX all-reduce / chunked row all-reduce
     comm.setdefault("tp_row_chunks", 2)
     comm.setdefault("sp_chunks", 2)             # SP all-gather / reduce-scatter chunks
-    comm.setdefault("wgrad_stream", "auto")     # wgrad GEMMs on a side stream (auto: hidden<=2048)
+    comm.setdefault("wgrad_stream", False)      # wgrad GEMMs on a side stream (opt-in, see eager_engine)
     comm.setdefault("overlap_optimizer_grid", 128)  # workgroups of the forward-overlapped AdamW
     eng = config.setdefault("Engine", AttrDict())
     eng.setdefault("cuda_graph", False)        # whole-step HIP graph (single rank)
