@@ -15,14 +15,16 @@
 //    lane^32 exchange, and the S^T accumulator is directly the B operand of
 //    O^T = V^T.P^T (no LDS round trip for P).
 //  * V^T fragments come from ds_read_b64_tr_b16 (hardware transpose).
-//  * K/V tiles are XOR-swizzled in LDS (conflict-free for both the b128 row
-//    reads and the tr_b16 reads; verified by tools/lds_bank_sim.py).
+//  * K/V tiles are stored as 8-row x 32-column subtiles with an in-group XOR
+//    (conflict-free for both the b128 row reads and the tr_b16 reads;
+//    verified by tools/lds_bank_sim.py), addressed by base + immediate.
 //  * K/V tiles go HBM -> LDS by global_load_lds (no VGPR staging, no
 //    ds_write pass); tile i+1 is in flight into the second LDS buffer while
 //    tile i computes, one vmcnt drain + barrier per tile.
 //  * blockIdx is remapped so the q-blocks of one (batch, head) run on one XCD
 //    (shared K/V stay in that XCD's L2); causal grids are issued heaviest
 //    block first across the XCD's heads (lpt_order).
+#include <cstdlib>
 #include <type_traits>
 
 #include "fx_common.h"
@@ -34,40 +36,68 @@ namespace {
 
 constexpr float LOG2E = 1.4426950408889634f;
 #define FA_DKDV_QT 32  // query rows per dK/dV tile
+#ifndef FA_FWD_WAVES_DEFAULT
+#define FA_FWD_WAVES_DEFAULT 4
+#endif
 constexpr float LN2 = 0.6931471805599453f;
 
-template <int D>
-__device__ __forceinline__ int swz(int row) {
-  if constexpr (D == 128) return ((row & 3) << 2) | ((row >> 2) & 3);
-  else return ((row >> 1) & 1) | (((row >> 2) & 1) << 1) | ((((row >> 1) ^ (row >> 3)) & 1) << 2);
-}
-// byte offset of 16-byte chunk `ch` of `row` in a [rows][D] 16-bit tile image
+// LDS image of a [rows][D] 16-bit tile: 8-row x 32-column subtiles of 512 B,
+// the 16-byte chunk index XORed inside its 4-chunk group by (row>>2)&3.
+// Conflict-free for the b128 row reads of the 32x32x16 operand and for the
+// tr_b16 transposed reads (tools/lds_bank_sim.py), and -- unlike a whole-row
+// XOR -- the chunk GROUP (ch>>2) and the row group (row>>3) enter additively:
+// the reads of one tile then share a few per-lane base registers and differ
+// by immediates (ds_read offset:), instead of one address add per read.
 template <int D>
 __device__ __forceinline__ int loff(int row, int ch) {
-  return row * (D * 2) + ((ch ^ swz<D>(row)) << 4);
+  return (16 * D) * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) +
+         16 * ((ch & 3) ^ ((row >> 2) & 3));
+}
+// inverse: byte offset (16-byte aligned) -> (row, chunk)
+template <int D>
+__device__ __forceinline__ void linv(int o, int& row, int& ch) {
+  const int r8 = o / (16 * D), rem = o % (16 * D);
+  row = 8 * r8 + ((rem & 511) >> 6);
+  ch = 4 * (rem >> 9) + (((rem & 63) >> 4) ^ ((row >> 2) & 3));
 }
 
-// A/B fragment row read (32x32x16 operand): row r, k-step s, lane half h
+// Fragment reads of the 32x32x16 operands from a tile image, addressed as a
+// per-lane base (computed once per kernel) plus compile-time immediates:
+//  * row(tile, blk, s): A/B operand of rows 32*blk + (lane&31), k-step s
+//    (16 columns), lane half h = lane>>5 holding columns 8h..8h+7;
+//  * tr(tile, t, ss, dt): transposed operand via ds_read_b64_tr_b16 -- lane
+//    gets column dt*32 + (lane&31) of rows kb+{0..3} and kb+8+{0..3},
+//    kb = 32t + 16ss + 4h.
+// Both are loff() evaluated in closed form (checked against it for every
+// lane in tools/lds_bank_sim.py --check-frag).
 template <int D>
-__device__ __forceinline__ short8 row_frag(const char* tile, int row, int s, int h) {
-  return *reinterpret_cast<const short8*>(tile + loff<D>(row, 2 * s + h));
-}
-
-// Transposed fragment: lane gets column (dt*32 + (lane&31)) of rows
-// keybase+{0..3} and keybase+8+{0..3}; keybase includes 4*h.
-template <int D>
-__device__ __forceinline__ short8 tr_frag(const char* tile, int keybase, int dt, int lane) {
-  const int gi = (lane >> 4) & 1, i = lane & 15, q = i >> 2, p = i & 3;
-  const int ch = dt * 4 + 2 * gi + (p >> 1);
-  const int b0 = loff<D>(keybase + q, ch) + 8 * (p & 1);
-  const int b1 = loff<D>(keybase + 8 + q, ch) + 8 * (p & 1);
-  v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDSV4(tile + b0));
-  v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDSV4(tile + b1));
-  short8 r;
-  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-  return r;
-}
+struct Frag {
+  int rb0, rb1, tb0, tb1;
+  __device__ __forceinline__ void init(int lane) {
+    const int h = lane >> 5, r = lane & 31;
+    const int rbase = 16 * D * (r >> 3) + 64 * (r & 7);
+    rb0 = rbase + 16 * (h ^ ((r >> 2) & 3));
+    rb1 = rbase + 16 * ((2 + h) ^ ((r >> 2) & 3));
+    const int gi = (lane >> 4) & 1, q = (lane >> 2) & 3, p = lane & 3;
+    const int tbase = 64 * (4 * h + q) + 8 * (p & 1);
+    const int c = 2 * gi + (p >> 1);
+    tb0 = tbase + 16 * (c ^ h);
+    tb1 = tbase + 16 * (c ^ (2 + h)) + 16 * D;
+  }
+  __device__ __forceinline__ short8 row(const char* tile, int blk, int s) const {
+    return *reinterpret_cast<const short8*>(tile + ((s & 1) ? rb1 : rb0) + 64 * D * blk +
+                                            512 * (s >> 1));
+  }
+  __device__ __forceinline__ short8 tr(const char* tile, int t, int ss, int dt) const {
+    const int o = 64 * D * t + 32 * D * ss + 512 * dt;
+    v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDSV4(tile + tb0 + o));
+    v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDSV4(tile + tb1 + o));
+    short8 r;
+    r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+    r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+    return r;
+  }
+};
 
 // bf16 or fp16 inputs (T), fp32 accumulate; the 16-bit operands travel as raw lanes
 template <typename T>
@@ -95,19 +125,19 @@ __device__ __forceinline__ int crow(int i, int h) { return (i & 3) + 8 * (i >> 2
 // side is lane-linear, so the XOR swizzle is applied to the per-lane GLOBAL
 // source address (rule: swizzle both sides or neither).  Rows past `nvalid`
 // are clamped to the last valid row; the kernels mask them.
-template <int D, int ROWS>
+template <int D, int ROWS, int NW = 4>
 struct Glds {
   static constexpr int RB = D * 2;
-  static constexpr int NI = ROWS * RB / 1024 / 4;  // instructions per wave (4 waves)
+  static constexpr int NI = ROWS * RB / 1024 / NW;  // instructions per wave (NW waves)
+  static_assert(NI * 1024 * NW == ROWS * RB, "tile must split into 1 KiB pieces per wave");
   static __device__ __forceinline__ void load(const uint16_t* base, long stride, int row0,
                                               int nvalid, char* tile, int w, int lane) {
     const int last = nvalid - 1;
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
       const int blk = (w * NI + u) * 1024;
-      const int lin = blk + lane * 16;
-      const int row = lin / RB, chp = (lin % RB) >> 4;
-      const int chl = chp ^ swz<D>(row);
+      int row, chl;
+      linv<D>(blk + lane * 16, row, chl);
       int grow = row0 + row;
       grow = grow > last ? last : grow;
       const uint16_t* src = base + (long)grow * stride + chl * 8;
@@ -123,9 +153,9 @@ struct Glds {
 // scalar offset plus one 64-bit add per instruction instead of a 64-bit
 // multiply chain per lane per tile.  Partial (tail) tiles take the clamping
 // path above.
-template <int D, int ROWS>
+template <int D, int ROWS, int NW = 4>
 struct GldsStream {
-  using G = Glds<D, ROWS>;
+  using G = Glds<D, ROWS, NW>;
   const uint16_t* base;
   long stride;
   int nvalid, w;
@@ -137,9 +167,9 @@ struct GldsStream {
     w = wave;
 #pragma unroll
     for (int u = 0; u < G::NI; ++u) {
-      const int lin = (w * G::NI + u) * 1024 + lane * 16;
-      const int row = lin / G::RB, chp = (lin % G::RB) >> 4;
-      off[u] = (long)row * stride + (chp ^ swz<D>(row)) * 8;
+      int row, chl;
+      linv<D>((w * G::NI + u) * 1024 + lane * 16, row, chl);
+      off[u] = (long)row * stride + chl * 8;
     }
   }
   __device__ __forceinline__ void load(int row0, char* tile, int lane) const {
@@ -240,12 +270,14 @@ __device__ __forceinline__ void lpt_order(int lid, int nper, int BH, int& bh, in
 // ============================================================================
 // forward: WG = 4 waves x 32 queries = 128 queries; KV tile = 64 keys
 // ============================================================================
-template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
-__global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
+template <typename T, int D, bool CAUSAL, bool DROP, bool KB, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int KV = 64, TB = KV * D * 2;
+  constexpr int KV = 64, TB = KV * D * 2, QB = 32 * NW;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-  const int nq = (P.Sq + 127) / 128;
+  Frag<D> F;
+  F.init(lane);
+  const int nq = (P.Sq + QB - 1) / QB;
   const int nblk = nq * P.B * P.H;
   const int lid = xcd_remap(blockIdx.x, nblk);
   int bh, qblock;
@@ -265,7 +297,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
   int kv_len = P.Sk;
   if (P.kv_lens) kv_len = min(kv_len, P.kv_lens[b]);
 
-  const int wq0 = qblock * 128 + w * 32;
+  const int wq0 = qblock * QB + w * 32;
   const int qi = wq0 + (lane & 31);
   short8 qf[D / 16];
 #pragma unroll
@@ -277,7 +309,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
   }
 
   int kv_end = kv_len;
-  if (CAUSAL) kv_end = min(kv_end, (qblock + 1) * 128);
+  if (CAUSAL) kv_end = min(kv_end, (qblock + 1) * QB);
   const int ntiles = (kv_end + KV - 1) / KV;
 
   floatx16 oacc[D / 32];
@@ -289,7 +321,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
   const float sl2 = P.scale * LOG2E;
   const uint32_t cb = DROP ? attn_cb(P, bh) : 0u;
 
-  GldsStream<D, KV> kld, vld;
+  GldsStream<D, KV, NW> kld, vld;
   kld.init(kp, P.sk_s, kv_end, w, lane);
   vld.init(vp, P.sv_s, kv_end, w, lane);
   if (ntiles > 0) {
@@ -317,7 +349,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int s = 0; s < D / 16; ++s) kfr[t][s] = row_frag<D>(kt, 32 * t + (lane & 31), s, h);
+        for (int s = 0; s < D / 16; ++s) kfr[t][s] = F.row(kt, t, s);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
 #pragma unroll
@@ -326,49 +358,65 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
         for (int s = 0; s < D / 16; ++s) sacc[t] = mfma<T>(kfr[t][s], qf[s], sacc[t]);
       }
       const bool need_mask = (CAUSAL && kb + KV - 1 > wq0) || (kb + KV > kv_len);
-      float mloc = -INFINITY;
       if constexpr (KB) key_bias_add(sacc, P.kbias + (long)b * P.kb_b + kb, h, sl2);
+      // Online softmax on the lane's 32 scores.  Without a key bias the raw
+      // scores are maxed and the scale folds into one FMA before the exp2
+      // (scale > 0 commutes with max).  Only tiles on the causal diagonal or
+      // past kv_len run the per-element key index / compare / select pass
+      // (wave-uniform branch, masked scores set to -inf in place).
+      if (__builtin_expect(need_mask, 0)) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float x = KB ? sacc[t][i] : sacc[t][i] * sl2;
-          if (need_mask) {
+          for (int i = 0; i < 16; ++i) {
             const int key = kb + 32 * t + crow(i, h);
-            if ((CAUSAL && key > qi) || key >= kv_len) x = -INFINITY;
+            if ((CAUSAL && key > qi) || key >= kv_len) sacc[t][i] = -INFINITY;
           }
-          sacc[t][i] = x;
-          mloc = fmaxf(mloc, x);
-        }
-      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-      const float m_new = fmaxf(m_run, mloc);
-      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-      const float alpha = fexp2(m_run - m_use);
-      m_run = m_new;
-      lsum *= alpha;
-      // once every row max of the wave is settled alpha == 1 exactly: skip
-      // the 64-register rescale (wave-uniform branch)
-      if (__any(alpha != 1.f)) {
-#pragma unroll
-        for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
       }
+      {
+        float mloc = -INFINITY;
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int i = 0; i < 16; i += 2) {
-          float p0 = fexp2(sacc[t][i] - m_use), p1 = fexp2(sacc[t][i + 1] - m_use);
-          lsum += p0 + p1;
-          if (DROP) {
-            const int key = kb + 32 * t + crow(i, h);  // even
-            const uint32_t hh = lowbias32((((uint32_t)qi) << 16 | ((uint32_t)key >> 1)) ^ cb);
-            p0 = ((hh & 0xffffu) >= P.thr) ? p0 * P.drop_scale : 0.f;
-            p1 = ((hh >> 16) >= P.thr) ? p1 * P.drop_scale : 0.f;
-          }
-          sacc[t][i] = p0;
-          sacc[t][i + 1] = p1;
+          for (int i = 0; i < 16; ++i) mloc = fmaxf(mloc, sacc[t][i]);
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+        if constexpr (!KB) mloc *= sl2;
+        const float m_new = fmaxf(m_run, mloc);
+        const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+        const float alpha = fexp2(m_run - m_use);
+        m_run = m_new;
+        lsum *= alpha;
+        // once every row max of the wave is settled alpha == 1 exactly: skip
+        // the 64-register rescale (wave-uniform branch)
+        if (__any(alpha != 1.f)) {
+#pragma unroll
+          for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
         }
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; i += 2) {
+            float p0, p1;
+            if constexpr (KB) {
+              p0 = fexp2(sacc[t][i] - m_use);
+              p1 = fexp2(sacc[t][i + 1] - m_use);
+            } else {
+              p0 = fexp2(__builtin_fmaf(sacc[t][i], sl2, -m_use));
+              p1 = fexp2(__builtin_fmaf(sacc[t][i + 1], sl2, -m_use));
+            }
+            lsum += p0 + p1;
+            if (DROP) {  // the keep scale 1/(1-p) is applied once, to O
+              const int key = kb + 32 * t + crow(i, h);  // even
+              const uint32_t hh = lowbias32((((uint32_t)qi) << 16 | ((uint32_t)key >> 1)) ^ cb);
+              p0 = ((hh & 0xffffu) >= P.thr) ? p0 : 0.f;
+              p1 = ((hh >> 16) >= P.thr) ? p1 : 0.f;
+            }
+            sacc[t][i] = p0;
+            sacc[t][i + 1] = p1;
+          }
+      }
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -376,10 +424,9 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
           short8 pf;
 #pragma unroll
           for (int j = 0; j < 8; ++j) pf[j] = cvt16<T>(sacc[t][8 * ss + j]);
-          const int keybase = 32 * t + 16 * ss + 4 * h;
 #pragma unroll
           for (int dt = 0; dt < D / 32; ++dt)
-            oacc[dt] = mfma<T>(tr_frag<D>(vt, keybase, dt, lane), pf, oacc[dt]);
+            oacc[dt] = mfma<T>(F.tr(vt, t, ss, dt), pf, oacc[dt]);
         }
     }
     glds_wait();
@@ -387,7 +434,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnParams P) {
   }
 
   const float ltot = lsum + __shfl_xor(lsum, 32, 64);
-  const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
+  const float inv = ltot > 0.f ? (DROP ? P.drop_scale : 1.f) / ltot : 0.f;
   if (qi < P.Sq) {
     uint16_t* op = P.out + b * P.so_b + hd * P.so_h + (long)qi * P.so_s;
 #pragma unroll
@@ -441,6 +488,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KV = 64, TB = KV * D * 2;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  Frag<D> F;
+  F.init(lane);
   const int nq = (P.Sq + 127) / 128;
   const int nblk = nq * P.B * P.H;
   const int lid = xcd_remap(blockIdx.x, nblk);
@@ -519,8 +568,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
         for (int i = 0; i < 16; ++i) sacc[i] = dpacc[i] = 0.f;
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
-          sacc = mfma<T>(row_frag<D>(kt, 32 * t + (lane & 31), s, h), qf[s], sacc);
-          dpacc = mfma<T>(row_frag<D>(vt, 32 * t + (lane & 31), s, h), gf[s], dpacc);
+          sacc = mfma<T>(F.row(kt, t, s), qf[s], sacc);
+          dpacc = mfma<T>(F.row(vt, t, s), gf[s], dpacc);
         }
         if constexpr (KB) key_bias_add1(sacc, P.kbias + (long)b * P.kb_b + kb + 32 * t, h, sl2);
 #pragma unroll
@@ -546,10 +595,9 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
           short8 df;
 #pragma unroll
           for (int j = 0; j < 8; ++j) df[j] = cvt16<T>(sacc[8 * ss + j]);
-          const int keybase = 32 * t + 16 * ss + 4 * h;
 #pragma unroll
           for (int dt = 0; dt < D / 32; ++dt)
-            dqacc[dt] = mfma<T>(tr_frag<D>(kt, keybase, dt, lane), df, dqacc[dt]);
+            dqacc[dt] = mfma<T>(F.tr(kt, t, ss, dt), df, dqacc[dt]);
         }
       }
     }
@@ -602,6 +650,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
   constexpr int BUF = 2 * TB + 2 * QT * 4;
   char* vs = smem + 2 * BUF;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  Frag<D> F;
+  F.init(lane);
   const int nk = (P.Sk + 127) / 128;
   const int nblk = nk * P.B * P.H;
   const int lid = xcd_remap(blockIdx.x, nblk);
@@ -715,9 +765,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
         for (int i = 0; i < 16; ++i) sacc[i] = dpacc[i] = 0.f;
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
-          sacc = mfma<T>(row_frag<D>(qt, 32 * t + (lane & 31), s, h), kf[s], sacc);
-          dpacc = mfma<T>(row_frag<D>(gt, 32 * t + (lane & 31), s, h),
-                       row_frag<D>(vs, 32 * w + (lane & 31), s, h), dpacc);
+          sacc = mfma<T>(F.row(qt, t, s), kf[s], sacc);
+          dpacc = mfma<T>(F.row(gt, t, s), F.row(vs, w, s), dpacc);
         }
         // P o Z (for dV) and dS (for dK) straight to bf16, one 8-row half at a
         // time: no fp32 copies of the tile stay live across the MFMAs
@@ -735,11 +784,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
             pf[j] = cvt16<T>(p * z);
             df[j] = cvt16<T>(p * (dpacc[i] * z - dl_s[ql_]));  // dS
           }
-          const int qbase = 32 * t + 16 * ss + 4 * h;
 #pragma unroll
           for (int dt = 0; dt < D / 32; ++dt) {
-            dvacc[dt] = mfma<T>(tr_frag<D>(gt, qbase, dt, lane), pf, dvacc[dt]);
-            dkacc[dt] = mfma<T>(tr_frag<D>(qt, qbase, dt, lane), df, dkacc[dt]);
+            dvacc[dt] = mfma<T>(F.tr(gt, t, ss, dt), pf, dvacc[dt]);
+            dkacc[dt] = mfma<T>(F.tr(qt, t, ss, dt), df, dkacc[dt]);
           }
         }
       }
@@ -795,11 +843,38 @@ AttnParams make_params(const void* q, const void* k, const void* v, const long* 
 // Launch with dynamic LDS; above 64 KiB the kernel must opt in (up to the
 // 160 KiB of a CU).
 static void fa_launch(void (*kernel)(AttnParams), int grid, size_t smem, hipStream_t st,
-                      const AttnParams& P) {
+                      const AttnParams& P, int threads = 256) {
   if (smem > 65536)
     (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)smem);
-  hipLaunchKernelGGL(kernel, dim3(grid), dim3(256), smem, st, P);
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), smem, st, P);
+}
+
+// Forward workgroup width: NW waves x 32 queries share one K/V tile stream
+// (FLEETX_FA_FWD_WAVES = 4 or 8; see fwd_waves()).
+template <typename T, int D, int NW>
+static void fa_fwd_dispatch(bool causal, bool drop, bool kbias, int grid, size_t smem,
+                            hipStream_t st, const AttnParams& P) {
+  auto go = [&](void (*k)(AttnParams)) { fa_launch(k, grid, smem, st, P, 64 * NW); };
+  if (causal) {
+    if (drop) go(fa_fwd_kernel<T, D, true, true, false, NW>);
+    else go(fa_fwd_kernel<T, D, true, false, false, NW>);
+  } else if (kbias) {
+    if (drop) go(fa_fwd_kernel<T, D, false, true, true, NW>);
+    else go(fa_fwd_kernel<T, D, false, false, true, NW>);
+  } else {
+    if (drop) go(fa_fwd_kernel<T, D, false, true, false, NW>);
+    else go(fa_fwd_kernel<T, D, false, false, false, NW>);
+  }
+}
+
+static int fwd_waves() {
+  static int nw = [] {
+    const char* e = getenv("FLEETX_FA_FWD_WAVES");
+    const int v = e ? atoi(e) : FA_FWD_WAVES_DEFAULT;
+    return v == 8 ? 8 : 4;
+  }();
+  return nw;
 }
 
 #define FA_DISPATCH_D(KERNEL, DD, causal, drop, kbias, grid, smem, st, P)         \
@@ -841,10 +916,18 @@ static int flash_fwd_t(const void* q, const void* k, const void* v, void* out, f
   P.kbias = kbias;
   P.kb_b = kb_stride;
   P.so_b = os[0]; P.so_s = os[1]; P.so_h = os[2];
-  const int nq = (Sq + 127) / 128;
+  const int nw = fwd_waves();
+  const int nq = (Sq + 32 * nw - 1) / (32 * nw);
   const int grid = nq * B * H;
   const size_t smem = 4 * 64 * D * 2;
-  FA_DISPATCH(fa_fwd_kernel, D, causal, p > 0.f, kbias != nullptr, grid, smem, st, P);
+  const bool drop = p > 0.f, kb = kbias != nullptr;
+  if (nw == 8) {
+    if (D == 128) fa_fwd_dispatch<T, 128, 8>(causal, drop, kb, grid, smem, st, P);
+    else fa_fwd_dispatch<T, 64, 8>(causal, drop, kb, grid, smem, st, P);
+  } else {
+    if (D == 128) fa_fwd_dispatch<T, 128, 4>(causal, drop, kb, grid, smem, st, P);
+    else fa_fwd_dispatch<T, 64, 4>(causal, drop, kb, grid, smem, st, P);
+  }
   return 0;
 }
 
