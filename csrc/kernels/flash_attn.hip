@@ -572,23 +572,32 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
           dpacc = mfma<T>(F.row(vt, t, s), gf[s], dpacc);
         }
         if constexpr (KB) key_bias_add1(sacc, P.kbias + (long)b * P.kb_b + kb + 32 * t, h, sl2);
+        // masked scores -> -inf in place, on diagonal / tail tiles only
+        if (__builtin_expect(need_mask, 0)) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = kb + 32 * t + crow(i, h);
+            if ((CAUSAL && key > qi) || key >= kv_len) sacc[i] = -INFINITY;
+          }
+        }
+        const float sc = KB ? 1.f : sl2;
 #pragma unroll
         for (int i = 0; i < 16; i += 2) {
-          const int key = kb + 32 * t + crow(i, h);
-          const float sc = KB ? 1.f : sl2;
-          float p0 = fexp2(sacc[i] * sc - lse2), p1 = fexp2(sacc[i + 1] * sc - lse2);
-          if (need_mask) {
-            if ((CAUSAL && key > qi) || key >= kv_len) p0 = 0.f;
-            if ((CAUSAL && key + 1 > qi) || key + 1 >= kv_len) p1 = 0.f;
-          }
+          // invalid query rows carry lse2 = +inf: p = exp2(-inf) = 0
+          const float p0 = fexp2(__builtin_fmaf(sacc[i], sc, -lse2));
+          const float p1 = fexp2(__builtin_fmaf(sacc[i + 1], sc, -lse2));
           float dp0 = dpacc[i], dp1 = dpacc[i + 1];
           if (DROP) {
+            const int key = kb + 32 * t + crow(i, h);
             const uint32_t hh = lowbias32((((uint32_t)qi) << 16 | ((uint32_t)key >> 1)) ^ cb);
-            dp0 = ((hh & 0xffffu) >= P.thr) ? dp0 * P.drop_scale : 0.f;
-            dp1 = ((hh >> 16) >= P.thr) ? dp1 * P.drop_scale : 0.f;
+            dp0 = ((hh & 0xffffu) >= P.thr) ? dp0 : 0.f;
+            dp1 = ((hh >> 16) >= P.thr) ? dp1 : 0.f;
+            sacc[i] = p0 * __builtin_fmaf(dp0, P.drop_scale, -dlt);
+            sacc[i + 1] = p1 * __builtin_fmaf(dp1, P.drop_scale, -dlt);
+          } else {
+            sacc[i] = p0 * (dp0 - dlt);
+            sacc[i + 1] = p1 * (dp1 - dlt);
           }
-          sacc[i] = p0 * (dp0 - dlt);
-          sacc[i + 1] = p1 * (dp1 - dlt);
         }
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
@@ -673,7 +682,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
   const int wk0 = kblock * 128 + w * 32;
   const int ki = wk0 + (lane & 31);
   const bool kvalid = ki < kv_len;
-  const float kb2 = KB ? P.kbias[(long)b * P.kb_b + ki] * LOG2E : 0.f;
+  // per-key additive term of the exp2 argument; -inf masks keys past kv_len
+  const float kb2 = !kvalid ? -INFINITY : (KB ? P.kbias[(long)b * P.kb_b + ki] * LOG2E : 0.f);
   short8 kf[D / 16];
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) {
@@ -760,9 +770,19 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
             keep |= (r1 >= P.thr ? 1u : 0u) << (i + 1);
           }
         }
+        // causal: only the 32-query slices that cross this wave's keys need
+        // the per-element mask; it enters as the S accumulator's initial
+        // value (-inf where key > query), before any tile register is live.
+        // Keys past kv_len carry kb2 = -inf and query rows past Sq carry
+        // lse = +inf, so their p is exp2(-inf) = 0 without a compare.
         floatx16 sacc, dpacc;
 #pragma unroll
         for (int i = 0; i < 16; ++i) sacc[i] = dpacc[i] = 0.f;
+        if (CAUSAL && __builtin_expect(q0 < wk0 + 31, 0)) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (ki > q0 + crow(i, h)) sacc[i] = -INFINITY;
+        }
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
           sacc = mfma<T>(F.row(qt, t, s), kf[s], sacc);
@@ -777,12 +797,15 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
           for (int j = 0; j < 8; ++j) {
             const int i = 8 * ss + j;
             const int ql_ = 32 * t + crow(i, h);
-            const int q = qb + ql_;
-            float p = fexp2(sacc[i] * sl2 + kb2 - lse_s[ql_]);
-            if ((CAUSAL && ki > q) || !kvalid || q >= P.Sq) p = 0.f;
-            const float z = DROP ? (((keep >> i) & 1u) ? P.drop_scale : 0.f) : 1.f;
-            pf[j] = cvt16<T>(p * z);
-            df[j] = cvt16<T>(p * (dpacc[i] * z - dl_s[ql_]));  // dS
+            const float p = fexp2(__builtin_fmaf(sacc[i], sl2, kb2 - lse_s[ql_]));
+            if (DROP) {
+              const float z = ((keep >> i) & 1u) ? P.drop_scale : 0.f;
+              pf[j] = cvt16<T>(p * z);
+              df[j] = cvt16<T>(p * (dpacc[i] * z - dl_s[ql_]));  // dS
+            } else {
+              pf[j] = cvt16<T>(p);
+              df[j] = cvt16<T>(p * (dpacc[i] - dl_s[ql_]));  // dS
+            }
           }
 #pragma unroll
           for (int dt = 0; dt < D / 32; ++dt) {
