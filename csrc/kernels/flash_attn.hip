@@ -128,13 +128,20 @@ __device__ __forceinline__ int crow(int i, int h) { return (i & 3) + 8 * (i >> 2
 template <int D, int ROWS, int NW = 4>
 struct Glds {
   static constexpr int RB = D * 2;
-  static constexpr int NI = ROWS * RB / 1024 / NW;  // instructions per wave (NW waves)
-  static_assert(NI * 1024 * NW == ROWS * RB, "tile must split into 1 KiB pieces per wave");
+  static constexpr int NP = ROWS * RB / 1024;       // 1 KiB pieces in the tile
+  static constexpr int NI = (NP + NW - 1) / NW;     // instructions per wave (NW waves)
+  static_assert(NP * 1024 == ROWS * RB, "tile must split into 1 KiB pieces");
+  // wave w loads pieces w*NI .. w*NI+NI-1 (the last waves fewer when NW does
+  // not divide NP, e.g. 32 rows of D = 96); wave-uniform guard
+  static __device__ __forceinline__ bool has(int w, int u) {
+    return NP % NW == 0 || w * NI + u < NP;
+  }
   static __device__ __forceinline__ void load(const uint16_t* base, long stride, int row0,
                                               int nvalid, char* tile, int w, int lane) {
     const int last = nvalid - 1;
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
+      if (!has(w, u)) continue;
       const int blk = (w * NI + u) * 1024;
       int row, chl;
       linv<D>(blk + lane * 16, row, chl);
@@ -180,7 +187,8 @@ struct GldsStream {
     const uint16_t* tb = base + (long)row0 * stride;
 #pragma unroll
     for (int u = 0; u < G::NI; ++u)
-      __builtin_amdgcn_global_load_lds((const void*)(tb + off[u]),
+      if (G::has(w, u))
+        __builtin_amdgcn_global_load_lds((const void*)(tb + off[u]),
                                        (__attribute__((address_space(3))) void*)(
                                            tile + (w * G::NI + u) * 1024),
                                        16, 0, 0);
@@ -457,13 +465,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
 // ============================================================================
 template <typename T, int D>
 __global__ __launch_bounds__(256) void fa_bwd_pre_kernel(AttnParams P) {
-  // 8 threads x 16B per row chunk of 64 elems; D/8 threads per row
-  constexpr int TPR = D / 8;
+  // 8 elements (16 B) per thread; TPR = D/8 rounded up to a power of two
+  // threads per row (the extra threads of D = 96 contribute 0)
+  constexpr int TPR = D / 8 <= 8 ? 8 : 16;
   const long row = (long)blockIdx.x * (256 / TPR) + threadIdx.x / TPR;
   const int c = (threadIdx.x % TPR) * 8;
   const long total = (long)P.B * P.H * P.Sq;
   float s = 0.f;
-  if (row < total) {
+  if (row < total && c < D) {
     const int q = row % P.Sq;
     const int bh = row / P.Sq;
     const int b = bh / P.H, hd = bh % P.H;
@@ -918,6 +927,7 @@ static int fwd_waves() {
 #define FA_DISPATCH(KERNEL, D, causal, drop, kbias, grid, smem, st, P)                  \
   do {                                                                                  \
     if (D == 128) FA_DISPATCH_D(KERNEL, 128, causal, drop, kbias, grid, smem, st, P);   \
+    else if (D == 96) FA_DISPATCH_D(KERNEL, 96, causal, drop, kbias, grid, smem, st, P); \
     else FA_DISPATCH_D(KERNEL, 64, causal, drop, kbias, grid, smem, st, P);             \
   } while (0)
 
@@ -930,7 +940,7 @@ static int flash_fwd_t(const void* q, const void* k, const void* v, void* out, f
                             const int* kv_lens, const float* kbias, long kb_stride, int B, int H,
                             int Sq, int Sk, int D, int causal, float scale, float p, uint64_t key,
                             hipStream_t st) {
-  if (D != 64 && D != 128) return -1;
+  if (D != 64 && D != 96 && D != 128) return -1;
   if (kbias && (causal || kb_stride < ((Sk + 127) / 128) * 128)) return -2;
   AttnParams P = make_params(q, k, v, qs, ks, vs, B, H, Sq, Sk, scale, p, key);
   P.out = (uint16_t*)out;
@@ -939,7 +949,7 @@ static int flash_fwd_t(const void* q, const void* k, const void* v, void* out, f
   P.kbias = kbias;
   P.kb_b = kb_stride;
   P.so_b = os[0]; P.so_s = os[1]; P.so_h = os[2];
-  const int nw = fwd_waves();
+  const int nw = D == 96 ? 4 : fwd_waves();
   const int nq = (Sq + 32 * nw - 1) / (32 * nw);
   const int grid = nq * B * H;
   const size_t smem = 4 * 64 * D * 2;
@@ -949,6 +959,7 @@ static int flash_fwd_t(const void* q, const void* k, const void* v, void* out, f
     else fa_fwd_dispatch<T, 64, 8>(causal, drop, kb, grid, smem, st, P);
   } else {
     if (D == 128) fa_fwd_dispatch<T, 128, 4>(causal, drop, kb, grid, smem, st, P);
+    else if (D == 96) fa_fwd_dispatch<T, 96, 4>(causal, drop, kb, grid, smem, st, P);
     else fa_fwd_dispatch<T, 64, 4>(causal, drop, kb, grid, smem, st, P);
   }
   return 0;
@@ -963,7 +974,7 @@ static int flash_bwd_t(const void* q, const void* k, const void* v, const void* 
                             const float* kbias, long kb_stride, int B, int H,
                             int Sq, int Sk, int D, int causal, float scale, float p, uint64_t key,
                             hipStream_t st) {
-  if (D != 64 && D != 128) return -1;
+  if (D != 64 && D != 96 && D != 128) return -1;
   if (kbias && (causal || kb_stride < ((Sk + 127) / 128) * 128)) return -2;
   AttnParams P = make_params(q, k, v, qs, ks, vs, B, H, Sq, Sk, scale, p, key);
   P.o = (const uint16_t*)o;
@@ -981,9 +992,10 @@ static int flash_bwd_t(const void* q, const void* k, const void* v, const void* 
   P.sdq_b = dqs[0]; P.sdq_s = dqs[1]; P.sdq_h = dqs[2];
   {
     const long rows = (long)B * H * Sq;
-    const int rpb = 256 / (D / 8);
+    const int rpb = 256 / (D / 8 <= 8 ? 8 : 16);  // rows per block (fa_bwd_pre_kernel TPR)
     const int grid = (int)((rows + rpb - 1) / rpb);
     if (D == 128) fa_bwd_pre_kernel<T, 128><<<grid, 256, 0, st>>>(P);
+    else if (D == 96) fa_bwd_pre_kernel<T, 96><<<grid, 256, 0, st>>>(P);
     else fa_bwd_pre_kernel<T, 64><<<grid, 256, 0, st>>>(P);
   }
   {

@@ -11,8 +11,8 @@ a representation layer, truncated-normal position embedding.
 embedding for fine-tuning at another resolution.
 
 MI355X mapping: the patch embed is an unfold + GEMM (no conv), attention uses
-the fused non-causal flash kernel (head dims 64 / 128, other dims such as
-ViT-g's 88 zero-padded), LN and bias+GeLU(erf) are HIP kernels.
+the fused non-causal flash kernel (head dims 64 / 96 / 128, other dims such as
+ViT-g's 88 zero-padded to the 96 tile), LN and bias+GeLU(erf) are HIP kernels.
 """
 import math
 import os

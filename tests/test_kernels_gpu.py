@@ -152,7 +152,7 @@ def test_embedding():
 
 
 # ---------------------------------------------------------------- attention
-@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("D", [64, 96, 128])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_flash_attention(D, causal, p):
@@ -208,7 +208,7 @@ def test_decode_attention(dtype, D, nsplit):
     assert _rel(out.cpu(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("D", [64, 96, 128])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attention_fp16(D, causal):
     """fp16 flash forward + backward (f16 MFMA path) vs fp32."""
@@ -396,9 +396,9 @@ def test_gpt_train_step_loss_decreases():
     assert losses[-1] < losses[0] - 0.5, losses
 
 
-@pytest.mark.parametrize("D", [40, 88])
+@pytest.mark.parametrize("D", [40, 88, 112])
 def test_flash_attention_padded_head_dim(D):
-    """Head dims outside {64,128} (ViT-g: 88) go through zero-padded tiles."""
+    """Head dims outside {64,96,128} (ViT-g: 88 -> 96) go through zero-padded tiles."""
     from fleetx_amd import ops
     B, S, H = 2, 257, 4  # ViT-style odd token count (cls + 16x16 patches)
     q, k, v = [torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)

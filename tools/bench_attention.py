@@ -1,5 +1,7 @@
 """Fused attention micro-benchmark on MI355X (forward and backward, causal /
 non-causal, attention dropout on / off) at the GPT-3 6.7B training shape.
+Forward and backward are each timed over ``--iters`` back-to-back launches
+(no host gaps; matches rocprofv3 kernel time within a few percent).
 
 Prints one JSON line per case with milliseconds and achieved TFLOP/s
 (forward 4*B*H*S^2*D, backward 2.5x that, both halved when causal -- the
@@ -38,19 +40,24 @@ def main():
             for _ in range(3):
                 torch.autograd.grad(fwd(), qkv, g)
             torch.cuda.synchronize()
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-            tf = tb = 0.0
+            # back-to-back launches between two events: the host enqueues
+            # ahead of the GPU, so the time is the kernels' (no launch gaps)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
             for _ in range(args.iters):
-                ev[0].record()
-                o = fwd()
-                ev[1].record()
+                fwd()
+            e1.record()
+            torch.cuda.synchronize()
+            tf = e0.elapsed_time(e1) / args.iters
+            outs = [fwd() for _ in range(args.iters)]
+            torch.cuda.synchronize()
+            e0.record()
+            for o in outs:
                 torch.autograd.grad(o, qkv, g)
-                ev[2].record()
-                torch.cuda.synchronize()
-                tf += ev[0].elapsed_time(ev[1])
-                tb += ev[1].elapsed_time(ev[2])
-            tf /= args.iters
-            tb /= args.iters
+            e1.record()
+            torch.cuda.synchronize()
+            tb = e0.elapsed_time(e1) / args.iters
+            del outs
             flops = 4.0 * B * H * S * S * D * (0.5 if causal else 1.0)
             print(json.dumps({"B": B, "S": S, "H": H, "D": D, "dtype": args.dtype,
                               "causal": causal, "dropout": p,
