@@ -36,6 +36,9 @@ namespace {
 
 constexpr float LOG2E = 1.4426950408889634f;
 #define FA_DKDV_QT 32  // query rows per dK/dV tile
+#ifndef FA_RESCALE_THR
+#define FA_RESCALE_THR 8.0f  // log2 units; 0 = rescale on every growth
+#endif
 #ifndef FA_FWD_WAVES_DEFAULT
 #define FA_FWD_WAVES_DEFAULT 4
 #endif
@@ -389,19 +392,23 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
           for (int i = 0; i < 16; ++i) mloc = fmaxf(mloc, sacc[t][i]);
         mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
         if constexpr (!KB) mloc *= sl2;
-        const float m_new = fmaxf(m_run, mloc);
-        const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-        const float alpha = fexp2(m_run - m_use);
-        m_run = m_new;
-        lsum *= alpha;
-        // once every row max of the wave is settled alpha == 1 exactly: skip
-        // the 64-register rescale (wave-uniform branch)
-        if (__any(alpha != 1.f)) {
+        // Deferred rescale: the running max moves (and O / l are rescaled)
+        // only when some row of the wave grew by more than FA_RESCALE_THR
+        // (log2 units) -- otherwise p = exp2(s - m_run) stays <= 2^THR, exact
+        // in fp32 and as bf16 operands (same relative precision).  The
+        // decision precedes this tile's exp2, so O, l and P always share one
+        // reference max (tests/test_kernels_gpu.py forces the branch mid-row).
+        if (__any(mloc > m_run + FA_RESCALE_THR)) {
+          const float m_new = fmaxf(m_run, mloc);
+          const float alpha = fexp2(m_run - ((m_new == -INFINITY) ? 0.f : m_new));
+          m_run = m_new;
+          lsum *= alpha;
 #pragma unroll
           for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
             for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
         }
+        const float m_use = (m_run == -INFINITY) ? 0.f : m_run;
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll

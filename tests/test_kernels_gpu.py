@@ -173,6 +173,32 @@ def test_flash_attention(D, causal, p):
             qkv.grad[:, :, :, i], ref_in.grad[:, :, :, i]))
 
 
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_rescale_branch(causal):
+    """Deferred online-softmax rescale (FA_RESCALE_THR = 8, log2 units): one key
+    row whose scores jump ~13 log2 units mid-row forces the rescale branch at
+    a later tile, a second one (~6.5) grows the max WITHOUT a rescale (p up to
+    2^6.5 against the stale max).  Full-tensor fp32 reference, fwd + bwd."""
+    from fleetx_amd import ops
+    B, S, H, D = 1, 512, 2, 128
+    torch.manual_seed(7)
+    q = (0.5 * torch.randn(B, S, H, D, device=DEV)).abs()
+    k = 0.5 * torch.randn(B, S, H, D, device=DEV)
+    v = torch.randn(B, S, H, D, device=DEV)
+    k[:, 100] = 1.0   # +~6.5 in log2 units: below the threshold
+    k[:, 300] = 2.0   # +~13: forces the rescale inside the 5th 64-key tile
+    q, k, v = [t.bfloat16().requires_grad_() for t in (q, k, v)]
+    out = ops.flash_attention(q, k, v, causal=causal)
+    qr, kr, vr = [t.detach().float().requires_grad_() for t in (q, k, v)]
+    ref = ops.attention_reference(qr, kr, vr, causal=causal)
+    assert _rel(out, ref) < 2e-2, _rel(out, ref)
+    g = torch.randn_like(ref)
+    out.backward(g.bfloat16())
+    ref.backward(g)
+    for a, r in ((q, qr), (k, kr), (v, vr)):
+        assert _rel(a.grad, r.grad) < 3e-2, _rel(a.grad, r.grad)
+
+
 def test_flash_attention_tail_and_kvlens():
     from fleetx_amd import ops
     B, S, H, D = 2, 200, 2, 128
