@@ -123,6 +123,11 @@ __device__ __forceinline__ short cvt16(float x) {
 // row index (within a 32-row C tile) held in register i for lane half h
 __device__ __forceinline__ int crow(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
+// 16 zero bytes in global memory: the LDS-DMA source of tile columns past a
+// head dim that is not a tile width (D = 88 on the 96 tile, 40 on 64), so
+// q / k / v need no zero-padded copies.
+__device__ __attribute__((aligned(16))) uint16_t fa_zero16[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
 // Tile loader: ROWS x D 16-bit elements straight into the swizzled LDS image
 // with global_load_lds (16 B per lane, 1 KiB per wave-instruction).  The LDS
 // side is lane-linear, so the XOR swizzle is applied to the per-lane GLOBAL
@@ -140,7 +145,8 @@ struct Glds {
     return NP % NW == 0 || w * NI + u < NP;
   }
   static __device__ __forceinline__ void load(const uint16_t* base, long stride, int row0,
-                                              int nvalid, char* tile, int w, int lane) {
+                                              int nvalid, char* tile, int w, int lane,
+                                              int dv = D) {
     const int last = nvalid - 1;
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
@@ -150,7 +156,8 @@ struct Glds {
       linv<D>(blk + lane * 16, row, chl);
       int grow = row0 + row;
       grow = grow > last ? last : grow;
-      const uint16_t* src = base + (long)grow * stride + chl * 8;
+      // columns past the valid head dim (e.g. 88 of a 96 tile) read zeros
+      const uint16_t* src = chl * 8 < dv ? base + (long)grow * stride + chl * 8 : fa_zero16;
       __builtin_amdgcn_global_load_lds((const void*)src,
                                        (__attribute__((address_space(3))) void*)(tile + blk), 16,
                                        0, 0);
@@ -168,23 +175,28 @@ struct GldsStream {
   using G = Glds<D, ROWS, NW>;
   const uint16_t* base;
   long stride;
-  int nvalid, w;
+  int nvalid, w, dv;
+  unsigned zmask;  // bit u: this lane's piece u lies past the valid head dim
   long off[G::NI];
-  __device__ __forceinline__ void init(const uint16_t* b, long s, int nv, int wave, int lane) {
+  __device__ __forceinline__ void init(const uint16_t* b, long s, int nv, int wave, int lane,
+                                       int dvalid = D) {
     base = b;
     stride = s;
     nvalid = nv;
     w = wave;
+    dv = dvalid;
+    zmask = 0u;
 #pragma unroll
     for (int u = 0; u < G::NI; ++u) {
       int row, chl;
       linv<D>((w * G::NI + u) * 1024 + lane * 16, row, chl);
       off[u] = (long)row * stride + chl * 8;
+      if (chl * 8 >= dv) zmask |= 1u << u;
     }
   }
   __device__ __forceinline__ void load(int row0, char* tile, int lane) const {
-    if (row0 + ROWS > nvalid) {
-      G::load(base, stride, row0, nvalid, tile, w, lane);
+    if (row0 + ROWS > nvalid || dv < D) {  // tail tile / partial head dim (wave-uniform)
+      G::load(base, stride, row0, nvalid, tile, w, lane, dv);
       return;
     }
     const uint16_t* tb = base + (long)row0 * stride;
@@ -222,6 +234,7 @@ struct AttnParams {
   float scale;
   uint32_t klo, khi, thr;
   float drop_scale;
+  int dval;              // valid head dim (<= the tile's D; columns past it are zero)
   const uint64_t* salt;  // graph mode: per-replay device salt (fx_set_dropout_salt)
 };
 
@@ -313,7 +326,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
   short8 qf[D / 16];
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) {
-    if (qi < P.Sq)
+    if (qi < P.Sq && 16 * s + 8 * h < P.dval)
       qf[s] = *reinterpret_cast<const short8*>(qp + (long)qi * P.sq_s + 16 * s + 8 * h);
     else
       qf[s] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
@@ -333,8 +346,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
   const uint32_t cb = DROP ? attn_cb(P, bh) : 0u;
 
   GldsStream<D, KV, NW> kld, vld;
-  kld.init(kp, P.sk_s, kv_end, w, lane);
-  vld.init(vp, P.sv_s, kv_end, w, lane);
+  kld.init(kp, P.sk_s, kv_end, w, lane, P.dval);
+  vld.init(vp, P.sv_s, kv_end, w, lane, P.dval);
   if (ntiles > 0) {
     kld.load(0, smem, lane);
     vld.load(0, smem + 2 * TB, lane);
@@ -461,7 +474,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
         o.y = Elt<T>::from_f(oacc[dt][4 * g + 1] * inv);
         o.z = Elt<T>::from_f(oacc[dt][4 * g + 2] * inv);
         o.w = Elt<T>::from_f(oacc[dt][4 * g + 3] * inv);
-        *reinterpret_cast<ushort4*>(op + dt * 32 + 8 * g + 4 * h) = o;
+        if (dt * 32 + 8 * g + 4 * h < P.dval)
+          *reinterpret_cast<ushort4*>(op + dt * 32 + 8 * g + 4 * h) = o;
       }
     if (h == 0) P.lse[(long)bh * P.Sq + qi] = ltot > 0.f ? (m_run + log2f(ltot)) * LN2 : INFINITY;
   }
@@ -479,7 +493,7 @@ __global__ __launch_bounds__(256) void fa_bwd_pre_kernel(AttnParams P) {
   const int c = (threadIdx.x % TPR) * 8;
   const long total = (long)P.B * P.H * P.Sq;
   float s = 0.f;
-  if (row < total && c < D) {
+  if (row < total && c < P.dval) {
     const int q = row % P.Sq;
     const int bh = row / P.Sq;
     const int b = bh / P.H, hd = bh % P.H;
@@ -532,7 +546,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
   short8 qf[D / 16], gf[D / 16];
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) {
-    if (qvalid) {
+    if (qvalid && 16 * s + 8 * h < P.dval) {
       qf[s] = *reinterpret_cast<const short8*>(qp + (long)qi * P.sq_s + 16 * s + 8 * h);
       gf[s] = *reinterpret_cast<const short8*>(dop + (long)qi * P.so_s + 16 * s + 8 * h);
     } else {
@@ -556,8 +570,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
     for (int i = 0; i < 16; ++i) dqacc[dt][i] = 0.f;
 
   GldsStream<D, KV> kld, vld;
-  kld.init(kp, P.sk_s, kv_end, w, lane);
-  vld.init(vp, P.sv_s, kv_end, w, lane);
+  kld.init(kp, P.sk_s, kv_end, w, lane, P.dval);
+  vld.init(vp, P.sv_s, kv_end, w, lane, P.dval);
   if (ntiles > 0) {
     kld.load(0, smem, lane);
     vld.load(0, smem + 2 * TB, lane);
@@ -640,7 +654,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
         o.y = Elt<T>::from_f(dqacc[dt][4 * g + 1] * P.scale);
         o.z = Elt<T>::from_f(dqacc[dt][4 * g + 2] * P.scale);
         o.w = Elt<T>::from_f(dqacc[dt][4 * g + 3] * P.scale);
-        *reinterpret_cast<ushort4*>(dqp + dt * 32 + 8 * g + 4 * h) = o;
+        if (dt * 32 + 8 * g + 4 * h < P.dval)
+          *reinterpret_cast<ushort4*>(dqp + dt * 32 + 8 * g + 4 * h) = o;
       }
   }
 }
@@ -703,13 +718,13 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
   short8 kf[D / 16];
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) {
-    if (ki < P.Sk)
+    if (ki < P.Sk && 16 * s + 8 * h < P.dval)
       kf[s] = *reinterpret_cast<const short8*>(kp + (long)ki * P.sk_s + 16 * s + 8 * h);
     else
       kf[s] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
   }
   // V rows of this WG's 128 keys -> LDS (rows past Sk clamp; those keys are masked)
-  Glds<D, 128>::load(vp, P.sv_s, kblock * 128, P.Sk, vs, w, lane);
+  Glds<D, 128>::load(vp, P.sv_s, kblock * 128, P.Sk, vs, w, lane, P.dval);
   floatx16 dkacc[D / 32], dvacc[D / 32];
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt)
@@ -738,8 +753,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
     }
   };
   GldsStream<D, QT> qld, gld;
-  qld.init(qp, P.sq_s, P.Sq, w, lane);
-  gld.init(dop, P.so_s, P.Sq, w, lane);
+  qld.init(qp, P.sq_s, P.Sq, w, lane, P.dval);
+  gld.init(dop, P.so_s, P.Sq, w, lane, P.dval);
   if (ntiles > 0) {
     rowconst_load(q_begin);
     qld.load(q_begin, smem, lane);
@@ -851,8 +866,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
         c.y = Elt<T>::from_f(dvacc[dt][4 * g + 1]);
         c.z = Elt<T>::from_f(dvacc[dt][4 * g + 2]);
         c.w = Elt<T>::from_f(dvacc[dt][4 * g + 3]);
-        *reinterpret_cast<ushort4*>(dkp + dt * 32 + 8 * g + 4 * h) = a;
-        *reinterpret_cast<ushort4*>(dvp + dt * 32 + 8 * g + 4 * h) = c;
+        if (dt * 32 + 8 * g + 4 * h < P.dval)
+          *reinterpret_cast<ushort4*>(dkp + dt * 32 + 8 * g + 4 * h) = a;
+        if (dt * 32 + 8 * g + 4 * h < P.dval)
+          *reinterpret_cast<ushort4*>(dvp + dt * 32 + 8 * g + 4 * h) = c;
       }
   }
 }
@@ -907,6 +924,8 @@ static void fa_fwd_dispatch(bool causal, bool drop, bool kbias, int grid, size_t
   }
 }
 
+static int tile_dim(int d) { return d <= 64 ? 64 : (d <= 96 ? 96 : 128); }
+
 static int fwd_waves() {
   static int nw = [] {
     const char* e = getenv("FLEETX_FA_FWD_WAVES");
@@ -947,9 +966,13 @@ static int flash_fwd_t(const void* q, const void* k, const void* v, void* out, f
                             const int* kv_lens, const float* kbias, long kb_stride, int B, int H,
                             int Sq, int Sk, int D, int causal, float scale, float p, uint64_t key,
                             hipStream_t st) {
-  if (D != 64 && D != 96 && D != 128) return -1;
+  // D is the head dim of the tensors; the kernel runs the smallest tile width
+  // >= D (64 / 96 / 128) with the columns past D read as zeros
+  if (D % 8 || D <= 0 || D > 128) return -1;
   if (kbias && (causal || kb_stride < ((Sk + 127) / 128) * 128)) return -2;
   AttnParams P = make_params(q, k, v, qs, ks, vs, B, H, Sq, Sk, scale, p, key);
+  P.dval = D;
+  D = tile_dim(D);
   P.out = (uint16_t*)out;
   P.lse = lse;
   P.kv_lens = kv_lens;
@@ -981,9 +1004,11 @@ static int flash_bwd_t(const void* q, const void* k, const void* v, const void* 
                             const float* kbias, long kb_stride, int B, int H,
                             int Sq, int Sk, int D, int causal, float scale, float p, uint64_t key,
                             hipStream_t st) {
-  if (D != 64 && D != 96 && D != 128) return -1;
+  if (D % 8 || D <= 0 || D > 128) return -1;
   if (kbias && (causal || kb_stride < ((Sk + 127) / 128) * 128)) return -2;
   AttnParams P = make_params(q, k, v, qs, ks, vs, B, H, Sq, Sk, scale, p, key);
+  P.dval = D;
+  D = tile_dim(D);
   P.o = (const uint16_t*)o;
   P.dout = (const uint16_t*)dout;
   P.lse = const_cast<float*>(lse);

@@ -62,8 +62,9 @@ class _FlashAttn(torch.autograd.Function):
         # packed: None or the [B,S,H,3,D] tensor q/k/v are views of
         B, Sq, H, D = q.shape
         Sk = k.shape[1]
-        if D not in FLASH_DIMS:
-            raise NotImplementedError("flash attention supports head_dim 64/96/128 (got %d)" % D)
+        if not _native_dim(D):
+            raise NotImplementedError("flash attention supports head_dim multiples of 8 up to 128 "
+                                      "(got %d)" % D)
         for t in (q, k, v):
             if t.stride(-1) != 1:
                 raise ValueError("head dim must be contiguous")
@@ -178,17 +179,25 @@ FLASH_DIMS = (64, 96, 128)
 
 
 def _padded_dim(d):
-    """Smallest kernel head dim >= d: ViT-g's 88 runs the 96 tile (8 % zero
+    """Smallest kernel tile width >= d: ViT-g's 88 runs the 96 tile (8 % zero
     columns) instead of the 128 one (31 %)."""
     return next(x for x in FLASH_DIMS if x >= d)
+
+
+def _native_dim(d):
+    """Head dims the kernels take as they are: the tile columns past ``d`` are
+    read as zeros by the loaders and never stored (16-byte column chunks)."""
+    return 0 < d <= 128 and d % 8 == 0
 
 
 def flash_attention(q, k, v, causal=True, dropout_p=0.0, key=0, scale=None, kv_lens=None,
                     key_bias=None):
     """q: [B, Sq, H, D], k/v: [B, Sk, H, D] (strided views allowed).
 
-    Head dims other than 64/96/128 (e.g. ViT-g's 88 -> 96) are zero-padded to
-    the next kernel tile width: zero columns add nothing to QK^T and produce zero output
+    Head dims that are multiples of 8 up to 128 run natively on the next tile
+    width (ViT-g's 88 on the 96 tile: the loaders read the missing columns as
+    zeros, no padded copies).  Other dims <= 128 are zero-padded to the tile
+    width: zero columns add nothing to QK^T and produce zero output
     columns that are sliced off (the softmax scale keeps the true ``D``)."""
     D = q.shape[-1]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
@@ -196,7 +205,7 @@ def flash_attention(q, k, v, causal=True, dropout_p=0.0, key=0, scale=None, kv_l
         raise ValueError("key_bias is supported for non-causal attention only")
     if not q.is_cuda:
         return attention_reference(q, k, v, causal, dropout_p, key, scale, kv_lens, key_bias)
-    if D not in FLASH_DIMS:
+    if not _native_dim(D):
         if D > 128:
             # wider heads than one MFMA tile row: exact fp32 math path (S x S materialised)
             if not _WARNED.get(D):
@@ -217,7 +226,7 @@ def flash_attention_qkvpacked(qkv, causal=True, dropout_p=0.0, key=0, scale=None
     """qkv: [B, S, H, 3, D] -> out [B, S, H, D]; gradient lands in one packed buffer."""
     D = qkv.shape[-1]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
-    if not qkv.is_cuda or D not in FLASH_DIMS:
+    if not qkv.is_cuda or not _native_dim(D):
         return flash_attention(qkv[:, :, :, 0], qkv[:, :, :, 1], qkv[:, :, :, 2], causal,
                                dropout_p, key, scale, kv_lens, key_bias)
     if key_bias is not None and causal:

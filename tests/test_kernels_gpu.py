@@ -422,9 +422,10 @@ def test_gpt_train_step_loss_decreases():
     assert losses[-1] < losses[0] - 0.5, losses
 
 
-@pytest.mark.parametrize("D", [40, 88, 112])
+@pytest.mark.parametrize("D", [40, 88, 112, 100])
 def test_flash_attention_padded_head_dim(D):
-    """Head dims outside {64,96,128} (ViT-g: 88 -> 96) go through zero-padded tiles."""
+    """Head dims that are not a tile width: multiples of 8 (ViT-g: 88 on the 96
+    tile) run natively with zero-read columns, others (100) via padded copies."""
     from fleetx_amd import ops
     B, S, H = 2, 257, 4  # ViT-style odd token count (cls + 16x16 patches)
     q, k, v = [torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
