@@ -101,10 +101,11 @@ class Attention(nn.Module):
     def _core(self, x):
         B, N, C = x.shape
         qkv = _apply(self.qkv, x).view(B, N, 3, self.num_heads, self.head_dim)
-        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
         p = self.attn_drop if self.training else 0.0
         key = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
-        o = ops.flash_attention(q, k, v, causal=False, dropout_p=p, key=key, scale=self.scale)
+        # packed entry: dq / dk / dv written into one [B, N, 3, H, D] gradient
+        o = ops.flash_attention_qkvpacked(qkv, causal=False, dropout_p=p, key=key,
+                                          scale=self.scale, pack_dim=2)
         return o.reshape(B, N, C)
 
     def forward_nobias(self, x):

@@ -97,8 +97,10 @@ class _FlashAttn(torch.autograd.Function):
         Sk = k.shape[1]
         dout = dout.contiguous()
         if ctx.packed:
-            dqkv = torch.empty(B, Sq, H, 3, D, device=q.device, dtype=q.dtype)
-            dq, dk, dv = dqkv[:, :, :, 0], dqkv[:, :, :, 1], dqkv[:, :, :, 2]
+            pd = getattr(ctx, "pack_dim", 3)  # [B,S,H,3,D] (GPT) or [B,S,3,H,D] (ViT)
+            shape = (B, Sq, H, 3, D) if pd == 3 else (B, Sq, 3, H, D)
+            dqkv = torch.empty(shape, device=q.device, dtype=q.dtype)
+            dq, dk, dv = dqkv.select(pd, 0), dqkv.select(pd, 1), dqkv.select(pd, 2)
         else:
             dq = torch.empty(B, Sq, H, D, device=q.device, dtype=q.dtype)
             dk = torch.empty(B, Sk, H, D, device=q.device, dtype=q.dtype)
@@ -123,14 +125,15 @@ class _PackedEntry(torch.autograd.Function):
     """Routes the packed-QKV gradient back to the packed tensor."""
 
     @staticmethod
-    def forward(ctx, qkv, causal, p, key, scale, kv_lens, key_bias):
-        q, k, v = qkv[:, :, :, 0], qkv[:, :, :, 1], qkv[:, :, :, 2]
+    def forward(ctx, qkv, causal, p, key, scale, kv_lens, key_bias, pack_dim=3):
+        ctx.pack_dim = pack_dim
+        q, k, v = qkv.select(pack_dim, 0), qkv.select(pack_dim, 1), qkv.select(pack_dim, 2)
         return _FlashAttn.forward(ctx, q, k, v, qkv, causal, p, key, scale, kv_lens, key_bias)
 
     @staticmethod
     def backward(ctx, dout):
         grads = _FlashAttn.backward(ctx, dout)
-        return grads[3], None, None, None, None, None, None
+        return grads[3], None, None, None, None, None, None, None
 
 
 _WARNED = {}
@@ -222,16 +225,23 @@ def flash_attention(q, k, v, causal=True, dropout_p=0.0, key=0, scale=None, kv_l
 
 
 def flash_attention_qkvpacked(qkv, causal=True, dropout_p=0.0, key=0, scale=None, kv_lens=None,
-                              key_bias=None):
-    """qkv: [B, S, H, 3, D] -> out [B, S, H, D]; gradient lands in one packed buffer."""
+                              key_bias=None, pack_dim=3):
+    """qkv: [B, S, H, 3, D] (``pack_dim=3``, GPT's per-head interleave) or
+    [B, S, 3, H, D] (``pack_dim=2``, ViT / timm) -> out [B, S, H, D].  The
+    q / k / v gradients land straight in one packed buffer of qkv's layout
+    (no per-slice zero fill + copy + add in autograd)."""
     D = qkv.shape[-1]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if pack_dim not in (2, 3):
+        raise ValueError("pack_dim must be 2 or 3")
     if not qkv.is_cuda or not _native_dim(D):
-        return flash_attention(qkv[:, :, :, 0], qkv[:, :, :, 1], qkv[:, :, :, 2], causal,
-                               dropout_p, key, scale, kv_lens, key_bias)
+        return flash_attention(qkv.select(pack_dim, 0), qkv.select(pack_dim, 1),
+                               qkv.select(pack_dim, 2), causal, dropout_p, key, scale, kv_lens,
+                               key_bias)
     if key_bias is not None and causal:
         raise ValueError("key_bias is supported for non-causal attention only")
-    return _PackedEntry.apply(qkv, causal, float(dropout_p), key, scale, kv_lens, key_bias)
+    return _PackedEntry.apply(qkv, causal, float(dropout_p), key, scale, kv_lens, key_bias,
+                              pack_dim)
 
 
 def decode_splits(B, H, maxlen, target_wgs=2048, min_chunk=512):

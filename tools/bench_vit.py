@@ -4,7 +4,7 @@ step (forward, backward, global-norm clip, AdamW) through the engine, on
 synthetic images and random-init weights.
 
     python tools/bench_vit.py [--config fleetx_amd/configs/vis/vit/ViT_g_patch14_224_synthetic_dp8.yaml]
-        [--steps 10 --warmup 3] [--no-recompute] [-o Key=value ...]
+        [--steps 10 --warmup 3] [--recompute | --no-recompute] [-o Key=value ...]
 
 Model FLOPs per image = 3 x forward (no recompute term, as the GPT MFU):
 forward per token and layer = 2 x (4 h^2 + 2 h m) for the QKV / out / MLP
@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-recompute", action="store_true")
+    ap.add_argument("--recompute", action="store_true")
     ap.add_argument("-o", "--override", action="append", default=[])
     args = ap.parse_args()
     import torch
@@ -51,6 +52,8 @@ def main():
     ov = list(args.override)
     if args.no_recompute:
         ov.append("Model.use_recompute=False")
+    if args.recompute:
+        ov.append("Model.use_recompute=True")
     cfg = C.get_config(args.config, overrides=ov, nranks=1)
     lr = cfg.Optimizer.lr
     if lr.get("name") == "ViTLRScheduler":  # as tools/train.py: steps per epoch from the data
