@@ -77,7 +77,7 @@ int fx_gemm(int, int, int, int, int, int, int, const void*, long, const void*, l
 void fx_gemm_set_variant(int);
 int fx_decode_gemv(int, int, int, int, int, const void*, long, const void*, long, const void*,
                    const void*, long, void*, long, void*, void*, const long*, int, int, int,
-                   hipStream_t);
+                   const void*, const void*, float, hipStream_t);
 void fx_set_dropout_salt(const void*);
 void fx_set_adamw_lr_ptr(const void*);
 int fx_comm_max_world();
@@ -261,10 +261,11 @@ PYBIND11_MODULE(_kernels, m) {
   // decode-time skinny GEMM with fused sub-layer epilogues (decode_gemv.hip)
   m.def("decode_gemv", [](int dt, int epi, int M, int N, int K, ptr x, long ldx, ptr w, long ldw,
                           ptr bias, ptr res, long ldres, ptr y, long ldy, ptr kc, ptr vc, ptr pos,
-                          int heads, int head_dim, int maxlen, ptr st) {
+                          int heads, int head_dim, int maxlen, ptr ln_w, ptr ln_b, float ln_eps,
+                          ptr st) {
     return fx_decode_gemv(dt, epi, M, N, K, CP(x), ldx, CP(w), ldw, CP(bias), CP(res), ldres, P(y),
                           ldy, P(kc), P(vc), reinterpret_cast<const long*>(pos), heads, head_dim,
-                          maxlen, S(st));
+                          maxlen, CP(ln_w), CP(ln_b), ln_eps, S(st));
   });
   // graph mode: device-resident dropout salt / AdamW learning rate (0 = off)
   m.def("set_dropout_salt", [](ptr p) { fx_set_dropout_salt(CP(p)); });

@@ -47,11 +47,14 @@ template <> struct Elt<f16> {
 
 // Load / store 8 consecutive 16-bit elements as float[8].
 template <typename T>
-__device__ __forceinline__ void load8(const uint16_t* p, float* f) {
-  uint4 v = *reinterpret_cast<const uint4*>(p);
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
   const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] = Elt<T>::to_f(h[j]);
+}
+template <typename T>
+__device__ __forceinline__ void load8(const uint16_t* p, float* f) {
+  unpack8<T>(*reinterpret_cast<const uint4*>(p), f);
 }
 template <typename T>
 __device__ __forceinline__ void store8(uint16_t* p, const float* f) {

@@ -178,25 +178,34 @@ def _fusable(layer):
 
 
 def _layer_decode_fused(layer, x, cache, li, pos, lens_after):
-    """One-token pass as five kernels (K19, the fused_multi_transformer
-    counterpart): LN1 -> [QKV GEMV + bias, K/V appended to the cache in the
-    epilogue] -> split-K decode attention -> [out-proj GEMV + bias + residual]
-    -> LN2 -> [FFN1 GEMV + bias + GeLU] -> [FFN2 GEMV + bias + residual].
-    Returns None when a GEMV does not cover the shape (batch > 16)."""
+    """One-token pass as four GEMV launches and the attention (K19, the
+    fused_multi_transformer counterpart): [LN1 + QKV GEMV + bias, K/V appended
+    to the cache in the epilogue] -> split-K decode attention -> [out-proj
+    GEMV + bias + residual] -> [LN2 + FFN1 GEMV + bias + GeLU] -> [FFN2 GEMV +
+    bias + residual].  The LayerNorms run as GEMV prologues (each block
+    normalises the few rows into LDS); shapes the fused prologue does not
+    cover fall back to a separate LayerNorm launch.  Returns None when a GEMV
+    does not cover the shape (batch > 16)."""
     from ....ops import gemm as G
     attn, mlp = layer.attn, layer.mlp
     B, h = x.shape[0], x.shape[-1]
     x2d = x.reshape(B, h)
-    hn = layer.ln1(x2d)
-    q = G.decode_linear(hn, attn.qkv_proj.weight, attn.qkv_proj.bias, G.GV_QKV,
-                        qkv_cache=(cache.k[li], cache.v[li], pos))
+    kv = (cache.k[li], cache.v[li], pos)
+    q = G.decode_linear(x2d, attn.qkv_proj.weight, attn.qkv_proj.bias, G.GV_QKV, qkv_cache=kv,
+                        ln=(layer.ln1.weight, layer.ln1.bias, layer.ln1.eps))
+    if q is None:
+        q = G.decode_linear(layer.ln1(x2d), attn.qkv_proj.weight, attn.qkv_proj.bias, G.GV_QKV,
+                            qkv_cache=kv)
     if q is None:
         return None
     o = ops.decode_attention(q.view(B, attn.heads, attn.head_dim), cache.k[li], cache.v[li],
                              lens_after)
     x2 = G.decode_linear(o.view(B, -1), attn.out_proj.weight, attn.out_proj.bias, G.GV_RES,
                          res=x2d)
-    f = G.decode_linear(layer.ln2(x2), mlp.fc1.weight, mlp.fc1.bias, G.GV_GELU)
+    f = G.decode_linear(x2, mlp.fc1.weight, mlp.fc1.bias, G.GV_GELU,
+                        ln=(layer.ln2.weight, layer.ln2.bias, layer.ln2.eps))
+    if f is None:
+        f = G.decode_linear(layer.ln2(x2), mlp.fc1.weight, mlp.fc1.bias, G.GV_GELU)
     out = G.decode_linear(f, mlp.fc2.weight, mlp.fc2.bias, G.GV_RES, res=x2)
     return out.view(B, 1, h)
 

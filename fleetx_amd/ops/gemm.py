@@ -183,12 +183,16 @@ def wgrad_16(dy2, x2):
 GV_BIAS, GV_GELU, GV_RES, GV_QKV = range(4)
 
 
-def decode_linear(x, weight, bias=None, epi=GV_BIAS, res=None, qkv_cache=None):
+def decode_linear(x, weight, bias=None, epi=GV_BIAS, res=None, qkv_cache=None, ln=None):
     """``x [M, K] @ weight[N, K]^T`` for M <= 16 rows on the weight-streaming
     MFMA GEMV, with the epilogue ``epi``: GV_BIAS (+b), GV_GELU (gelu_tanh(+b)),
     GV_RES (+b + res[M, N]) or GV_QKV (``qkv_cache = (k_cache, v_cache, pos)``:
     the packed [heads][3][head_dim] output is scattered -- q returned as [M, H*D],
     k/v written into the caches [M, maxlen, H, D] at ``pos`` [M]).
+
+    ``ln = (weight, bias, eps)`` (GV_GELU / GV_QKV): ``x`` is the residual
+    stream and its LayerNorm is fused into the GEMV as a prologue (the
+    decoder layer's LN1 / LN2 then cost no launch of their own).
 
     Returns the output, or None when the kernel does not cover the shape (the
     caller then uses the general GEMM)."""
@@ -202,6 +206,10 @@ def decode_linear(x, weight, bias=None, epi=GV_BIAS, res=None, qkv_cache=None):
         # it faster (tools/bench_gemv.py), and there is no epilogue to fuse
         return None
     if weight.dtype != x.dtype or weight.stride(1) != 1 or x.stride(1) != 1 or K % 1024:
+        return None
+    if ln is not None and (ln[0].dtype != x.dtype or ln[1] is None or ln[1].dtype != x.dtype
+                           or not ln[0].is_contiguous() or not ln[1].is_contiguous()
+                           or epi not in (GV_GELU, GV_QKV)):
         return None
     k = _lib.kernels()
     kc = vc = pos = None
@@ -220,7 +228,9 @@ def decode_linear(x, weight, bias=None, epi=GV_BIAS, res=None, qkv_cache=None):
                        weight.data_ptr(), weight.stride(0), _lib.ptr(bias), _lib.ptr(res),
                        res.stride(0) if res is not None else 0, y.data_ptr(), y.stride(0),
                        _lib.ptr(kc), _lib.ptr(vc), _lib.ptr(pos), heads, hd, maxlen,
-                       _lib.stream())
+                       _lib.ptr(ln[0]) if ln is not None else 0,
+                       _lib.ptr(ln[1]) if ln is not None else 0,
+                       float(ln[2]) if ln is not None else 0.0, _lib.stream())
     if nb == 0:
         return None
     _lib.maybe_sync()

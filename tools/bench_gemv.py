@@ -36,12 +36,20 @@ def main():
     args = ap.parse_args()
     from fleetx_amd.ops import gemm as G
     for name, (N, K) in SHAPES.items():
-        w = (torch.randn(N, K, device="cuda") * K ** -0.5).bfloat16()
+        # enough weight copies (>= 1 GiB) that successive calls stream from HBM,
+        # as in a decode step over all layers, not from the 256 MB Infinity Cache
+        ncopy = max(1, -(-(1 << 30) // (N * K * 2)))
+        ws = [(torch.randn(N, K, device="cuda") * K ** -0.5).bfloat16() for _ in range(ncopy)]
         b = torch.randn(N, device="cuda").bfloat16()
         for M in args.m:
             x = torch.randn(M, K, device="cuda").bfloat16()
-            us = timeit(lambda: G.decode_linear(x, w, b))
-            ub = timeit(lambda: F.linear(x, w, b))
+            it = [0]
+
+            def nxt():
+                it[0] = (it[0] + 1) % ncopy
+                return ws[it[0]]
+            us = timeit(lambda: G.decode_linear(x, nxt(), b))
+            ub = timeit(lambda: F.linear(x, nxt(), b))
             print(json.dumps({"shape": name, "M": M, "N": N, "K": K, 
                               "gemv_us": round(us, 2), "gemv_TB_s": round(N * K * 2 / us / 1e6, 2),
                               "hipblaslt_us": round(ub, 2),

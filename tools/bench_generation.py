@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--batch", type=int, nargs="+", default=[1, 8, 16])
     ap.add_argument("--prompt", type=int, default=128)
     ap.add_argument("--tokens", type=int, default=64)
+    ap.add_argument("--fused-only", action="store_true")
     args = ap.parse_args()
     from fleetx_amd.models.language_model.gpt.model import GPTConfig, GPTForPretraining
     from fleetx_amd.models.language_model.gpt.generation import GPTForGeneration
@@ -36,7 +37,7 @@ def main():
     nbytes = sum(p.numel() * p.element_size() for p in model.parameters())
     for B in args.batch:
         prompt = torch.randint(0, 50304, (B, args.prompt), device="cuda")
-        for fused in (False, True):
+        for fused in ((True,) if args.fused_only else (False, True)):
             gen = GPTForGeneration(model, {"max_dec_len": args.tokens, "fused_decode": fused,
                                            "decode_strategy": "greedy_search"})
             gen.generate(prompt, max_length=8)
