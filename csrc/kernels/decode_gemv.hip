@@ -339,10 +339,14 @@ int fx_decode_gemv(int dt, int epi, int M, int N, int K, const void* x, long ldx
   if (ln && (ln_b == nullptr || (epi != GV_GELU && epi != GV_QKV) || M > 1 ||
              (long)M * K * 2 > 96 * 1024))
     return 0;
-  // many column tiles: 8 waves per block, each on a shorter K range (more
-  // waves resident, shorter dependent chains); few tiles: 4 waves with two
-  // batches of loads in flight each (tools/bench_gemv.py)
-  const int ks = (N >= 8192 && K % 2048 == 0) ? 8 : 4;
+  static const int pin_ks = [] { const char* e = getenv("FLEETX_GEMV_KS"); return e ? atoi(e) : 0; }();
+  static const int pin_u = [] { const char* e = getenv("FLEETX_GEMV_U"); return e ? atoi(e) : 0; }();
+  // measured (tools/bench_gemv.py, M = 1, HBM-streamed weights): 4 waves with
+  // 4-chunk batches win on every GPT-3 1.3B / 6.7B layer and the LM head
+  // (1.3B FFN1 12.2 -> 8.8 us, LM head 57 -> 40 us = 5.2 TB/s); only the
+  // narrow N <= 2048 layers prefer 8 waves on shorter K ranges
+  int ks = (N <= 2048 && K % 2048 == 0) ? 8 : 4;
+  if ((pin_ks == 4 || pin_ks == 8) && K % (64 * 4 * pin_ks) == 0) ks = pin_ks;
   GemvArgs a;
   a.x = (const uint16_t*)x; a.w = (const uint16_t*)w; a.bias = (const uint16_t*)bias;
   a.res = (const uint16_t*)res; a.y = (uint16_t*)y;
@@ -351,7 +355,8 @@ int fx_decode_gemv(int dt, int epi, int M, int N, int K, const void* x, long ldx
   a.kc = (uint16_t*)kc; a.vc = (uint16_t*)vc; a.pos = pos;
   a.heads = heads; a.head_dim = head_dim; a.maxlen = maxlen;
   a.ln_w = (const uint16_t*)ln_w; a.ln_b = (const uint16_t*)ln_b; a.ln_eps = ln_eps;
-  const int u = (K / (64 * ks)) % 8 == 0 && K / (64 * ks) >= 16 ? 8 : 4;
+  int u = 4;
+  if (pin_u == 8 && (K / (64 * ks)) % 8 == 0) u = 8;
   const int rw = rows_per_block(N);
 #define FX_GV(T)                                                  \
   switch (epi) {                                                              \

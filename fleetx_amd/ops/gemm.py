@@ -201,10 +201,6 @@ def decode_linear(x, weight, bias=None, epi=GV_BIAS, res=None, qkv_cache=None, l
         return None
     M, K = x.shape
     N = weight.shape[0]
-    if epi == GV_BIAS and bias is None and N * K > 48 * 2 ** 20:
-        # a plain product of a large weight (e.g. the LM head): hipBLASLt streams
-        # it faster (tools/bench_gemv.py), and there is no epilogue to fuse
-        return None
     if weight.dtype != x.dtype or weight.stride(1) != 1 or x.stride(1) != 1 or K % 1024:
         return None
     if ln is not None and (ln[0].dtype != x.dtype or ln[1] is None or ln[1].dtype != x.dtype
