@@ -62,8 +62,20 @@ __global__ __launch_bounds__(256) void fake_quant_kernel(const uint16_t* __restr
 // Pass 2: one workgroup per (b, h) merges the nsplit partials.
 // Small-batch long-context decode thus spreads over B*H*nsplit >= ~2 waves of
 // workgroups instead of B*H (a few CUs out of 256).
-template <typename T, int D>
-__global__ __launch_bounds__(256) void decode_attn_split_kernel(
+// merge another online-softmax state (m2, l2, o2) into (m, l, o)
+__device__ __forceinline__ void merge_state(float& m, float& l, float* o, float m2, float l2,
+                                            const float* o2) {
+  const float M = fmaxf(m, m2);
+  if (M == -INFINITY) return;
+  const float a = __expf(m - M), c = __expf(m2 - M);
+  l = l * a + l2 * c;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = o[j] * a + o2[j] * c;
+  m = M;
+}
+
+template <typename T, int D, int NW>
+__global__ __launch_bounds__(64 * NW) void decode_attn_split_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int* __restrict__ lens, float* __restrict__ ws,
     int H, int nsplit, int chunk, long sqb, long sqh, long skb, long sks, long skh, float scale,
@@ -86,8 +98,10 @@ __global__ __launch_bounds__(256) void decode_attn_split_kernel(
   for (int j = 0; j < 8; ++j) o[j] = 0.f;
   const uint16_t* kb = kc + b * skb + hd * skh + c;
   const uint16_t* vb = vc + b * skb + hd * skh + c;
-  // wave w, step: keys k0 + u*KPW*4 + w*KPW + sub, u < U
-  for (int k0 = k_lo; k0 < k_hi; k0 += 4 * KPW * U) {
+  // wave w, step: keys k0 + u*KPW*NW + w*KPW + sub, u < U.  NW = 16 for few
+  // (batch, head) pairs: a whole short context is one step (one memory round
+  // trip) of one workgroup instead of several steps of 4 waves
+  for (int k0 = k_lo; k0 < k_hi; k0 += NW * KPW * U) {
     float sc[U];
     int key[U];
     // K and V rows of the step are loaded together (V does not depend on the
@@ -95,7 +109,7 @@ __global__ __launch_bounds__(256) void decode_attn_split_kernel(
     uint4 kraw[U], vraw[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      key[u] = k0 + (u * 4 + w) * KPW + sub;
+      key[u] = k0 + (u * NW + w) * KPW + sub;
       const int kk = key[u] < k_hi ? key[u] : k_lo;  // in-range dummy row
       kraw[u] = *reinterpret_cast<const uint4*>(kb + (long)kk * sks);
       vraw[u] = *reinterpret_cast<const uint4*>(vb + (long)kk * sks);
@@ -135,21 +149,35 @@ __global__ __launch_bounds__(256) void decode_attn_split_kernel(
     }
     m = mx;
   }
-  // merge the 4*KPW lane-group states of each column slice through LDS
-  __shared__ float sm_m[256], sm_l[256], sm_o[256][8];
-  sm_m[threadIdx.x] = m;
-  sm_l[threadIdx.x] = l;
+  // merge: the KPW lane groups of a wave share each column slice -> lane
+  // shuffles; then one state per (wave, slice) through LDS, NW-way
 #pragma unroll
-  for (int j = 0; j < 8; ++j) sm_o[threadIdx.x][j] = o[j];
+  for (int off = LPK; off < 64; off <<= 1) {
+    float o2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o2[j] = __shfl_xor(o[j], off, 64);
+    const float m2 = __shfl_xor(m, off, 64), l2 = __shfl_xor(l, off, 64);
+    merge_state(m, l, o, m2, l2, o2);
+  }
+  __shared__ float sm_m[NW * LPK], sm_l[NW * LPK], sm_o[NW * LPK][8];
+  if (lane < LPK) {
+    sm_m[w * LPK + lane] = m;
+    sm_l[w * LPK + lane] = l;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sm_o[w * LPK + lane][j] = o[j];
+  }
   __syncthreads();
   if (threadIdx.x < LPK) {
     float M = -INFINITY;
-    for (int t = threadIdx.x; t < 256; t += LPK) M = fmaxf(M, sm_m[t]);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) M = fmaxf(M, sm_m[i * LPK + threadIdx.x]);
     float L = 0.f, O[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) O[j] = 0.f;
     if (M != -INFINITY) {
-      for (int t = threadIdx.x; t < 256; t += LPK) {
+#pragma unroll
+      for (int i = 0; i < NW; ++i) {
+        const int t = i * LPK + threadIdx.x;
         if (sm_m[t] == -INFINITY) continue;
         const float a = __expf(sm_m[t] - M);
         L += sm_l[t] * a;
@@ -227,11 +255,19 @@ extern "C" int fx_decode_attn(int dt, const void* q, const void* kc, const void*
   if (nsplit < 1) return -2;
   const int chunk = (maxlen + nsplit - 1) / nsplit;
   const int g = B * H * nsplit;
+  // few workgroups (small batch x heads): 16 waves each, so a short context
+  // is one load step; many: 4 waves
+  const bool wide = g < 256;
 #define FX_DEC(TT, DD)                                                                           \
   do {                                                                                           \
-    decode_attn_split_kernel<TT, DD><<<g, 256, 0, st>>>(                                         \
-        (const uint16_t*)q, (const uint16_t*)kc, (const uint16_t*)vc, lens, ws, H, nsplit, chunk, \
-        sqb, sqh, skb, sks, skh, scale, (uint16_t*)out, sob);                                     \
+    if (wide)                                                                                    \
+      decode_attn_split_kernel<TT, DD, 16><<<g, 1024, 0, st>>>(                                  \
+          (const uint16_t*)q, (const uint16_t*)kc, (const uint16_t*)vc, lens, ws, H, nsplit,     \
+          chunk, sqb, sqh, skb, sks, skh, scale, (uint16_t*)out, sob);                           \
+    else                                                                                         \
+      decode_attn_split_kernel<TT, DD, 4><<<g, 256, 0, st>>>(                                    \
+          (const uint16_t*)q, (const uint16_t*)kc, (const uint16_t*)vc, lens, ws, H, nsplit,     \
+          chunk, sqb, sqh, skb, sks, skh, scale, (uint16_t*)out, sob);                           \
     if (nsplit > 1)                                                                              \
       decode_attn_combine_kernel<TT, DD><<<B * H, DD, 0, st>>>(ws, (uint16_t*)out, H, nsplit, sob); \
   } while (0)

@@ -239,14 +239,16 @@ def test_flash_attention_tail_and_kvlens():
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("nsplit", [1, None, 7])
-def test_decode_attention(dtype, D, nsplit):
-    """Split-K decode vs fp32: ragged lengths, splits that end up empty."""
+@pytest.mark.parametrize("BH", [(3, 4), (8, 32)])
+def test_decode_attention(dtype, D, nsplit, BH):
+    """Split-K decode vs fp32: ragged lengths, splits that end up empty; few
+    (batch, head) pairs run the 16-wave workgroup, many the 4-wave one."""
     from fleetx_amd import ops
-    B, H, L = 3, 4, 1300
+    (B, H), L = BH, 1300
     q = torch.randn(B, H, D, device=DEV, dtype=dtype)
     kc = torch.randn(B, L, H, D, device=DEV, dtype=dtype)
     vc = torch.randn(B, L, H, D, device=DEV, dtype=dtype)
-    lens = torch.tensor([1300, 17, 700], device=DEV, dtype=torch.int32)
+    lens = torch.tensor([1300, 17, 700, 1, 64, 513, 999, 1299][:B], device=DEV, dtype=torch.int32)
     out = ops.decode_attention(q, kc, vc, lens, nsplit=nsplit)
     assert out.dtype == dtype
     ref = ops.decode_attention(q.cpu().float(), kc.cpu().float(), vc.cpu().float(), lens.cpu())
