@@ -182,7 +182,7 @@ __device__ __forceinline__ void ln_prologue(const GemvArgs& a, uint16_t* xs, flo
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         o[j] = (short)Elt<T>::from_f((v[j] - mean[m]) * rstd[m] * gw[j] + gb[j]);
-      *(__attribute__((address_space(3))) short8*)(xs + (long)m * K + c * 8) = o;
+      *(__attribute__((address_space(3))) short8*)(xs + (long)m * (K + 8) + c * 8) = o;
     }
   }
   __syncthreads();
@@ -216,7 +216,8 @@ __global__ __launch_bounds__(64 * GV_KS) void gemv_kernel(GemvArgs a) {
   const int nrow = min(n0 + (r % RW), a.N - 1);
   const uint16_t* wp = a.w + (long)nrow * a.ldw + kb + 16 * g;
   // x rows >= M read row M-1 (no per-load select: their D rows are never stored)
-  const uint16_t* xp = LN ? xs_dyn + (long)min(r, a.M - 1) * a.K + kb + 16 * g
+  // LN rows in LDS are K + 8 elements apart: the 16 lanes' rows fall on different banks
+  const uint16_t* xp = LN ? xs_dyn + (long)min(r, a.M - 1) * (a.K + 8) + kb + 16 * g
                           : a.x + (long)min(r, a.M - 1) * a.ldx + kb + 16 * g;
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
   const int nch = kw / 64;
@@ -275,7 +276,7 @@ __global__ __launch_bounds__(64 * GV_KS) void gemv_kernel(GemvArgs a) {
 template <typename T, int EPI, int RW, int LNR>
 void launch_u(const GemvArgs& a, int u, int ks, hipStream_t s) {
   const dim3 grid((a.N + RW - 1) / RW);
-  const size_t lds = LNR > 0 ? (size_t)a.M * a.K * 2 : 0;
+  const size_t lds = LNR > 0 ? (size_t)a.M * (a.K + 8) * 2 : 0;
   auto go = [&](void (*k)(GemvArgs), int threads) {
     if (lds > 65536)
       (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -301,7 +302,8 @@ void launch_rw(const GemvArgs& a, int u, int ks, int rw, hipStream_t s) {
 // LayerNorm-fused GEMV: row-count bucket of the unrolled prologue
 template <typename T, int EPI>
 void launch_ln(const GemvArgs& a, int u, int ks, int rw, hipStream_t s) {
-  launch_rw<T, EPI, 1>(a, u, ks, rw, s);  // M == 1 (host check)
+  if (a.M == 1) launch_rw<T, EPI, 1>(a, u, ks, rw, s);
+  else launch_rw<T, EPI, 4>(a, u, ks, rw, s);  // M <= 4 (host check)
 }
 
 // columns per block (FLEETX_GEMV_ROWS pins 16 / 8 / 4 for tools/bench_gemv.py sweeps)
@@ -332,12 +334,12 @@ int fx_decode_gemv(int dt, int epi, int M, int N, int K, const void* x, long ldx
                    const void* ln_w, const void* ln_b, float ln_eps, hipStream_t s) {
   if (M < 1 || M > 16 || K % 1024 != 0 || (ldx % 8) || (ldw % 8)) return 0;
   const bool ln = ln_w != nullptr;
-  // fused LayerNorm for one row (batch-1 decode, where the separate launch
-  // dominates); more rows take the LayerNorm kernel (the prologue's per-row
-  // statistics measured slower than one launch from 2 rows on:
-  // tools/bench_generation.py, docs/KERNELS.md)
-  if (ln && (ln_b == nullptr || (epi != GV_GELU && epi != GV_QKV) || M > 1 ||
-             (long)M * K * 2 > 96 * 1024))
+  // fused LayerNorm for up to 4 rows (small-batch decode, where the separate
+  // launch dominates: 1.3B decode 1.27 / 1.38 / 1.43 -> 1.11 / 1.30 / 1.38 ms per
+  // token at batch 1 / 2 / 4); more rows take the LayerNorm kernel (a 16-row
+  // prologue measured 1.38 -> 2.13 ms at batch 8)
+  if (ln && (ln_b == nullptr || (epi != GV_GELU && epi != GV_QKV) || M > 4 ||
+             (long)M * (K + 8) * 2 > 96 * 1024))
     return 0;
   static const int pin_ks = [] { const char* e = getenv("FLEETX_GEMV_KS"); return e ? atoi(e) : 0; }();
   static const int pin_u = [] { const char* e = getenv("FLEETX_GEMV_U"); return e ? atoi(e) : 0; }();

@@ -18,6 +18,7 @@ MI355X design (K18/K19):
 * per-token attention uses the split-free decode kernel
   (``ops.decode_attention``) that streams the cache once.
 """
+import os
 import torch
 import torch.nn.functional as F
 
@@ -177,6 +178,10 @@ def _fusable(layer):
             and type(m.fc2) is L.RowParallelLinear)
 
 
+# LayerNorm as a GEMV prologue in the fused decode layer (FLEETX_DECODE_LN_FUSE=0: separate launch)
+_LN_FUSE = os.environ.get("FLEETX_DECODE_LN_FUSE", "1") == "1"
+
+
 def _layer_decode_fused(layer, x, cache, li, pos, lens_after):
     """One-token pass as four GEMV launches and the attention (K19, the
     fused_multi_transformer counterpart): [LN1 + QKV GEMV + bias, K/V appended
@@ -192,7 +197,7 @@ def _layer_decode_fused(layer, x, cache, li, pos, lens_after):
     x2d = x.reshape(B, h)
     kv = (cache.k[li], cache.v[li], pos)
     q = G.decode_linear(x2d, attn.qkv_proj.weight, attn.qkv_proj.bias, G.GV_QKV, qkv_cache=kv,
-                        ln=(layer.ln1.weight, layer.ln1.bias, layer.ln1.eps))
+                        ln=(layer.ln1.weight, layer.ln1.bias, layer.ln1.eps)) if _LN_FUSE else None
     if q is None:
         q = G.decode_linear(layer.ln1(x2d), attn.qkv_proj.weight, attn.qkv_proj.bias, G.GV_QKV,
                             qkv_cache=kv)
@@ -203,7 +208,7 @@ def _layer_decode_fused(layer, x, cache, li, pos, lens_after):
     x2 = G.decode_linear(o.view(B, -1), attn.out_proj.weight, attn.out_proj.bias, G.GV_RES,
                          res=x2d)
     f = G.decode_linear(x2, mlp.fc1.weight, mlp.fc1.bias, G.GV_GELU,
-                        ln=(layer.ln2.weight, layer.ln2.bias, layer.ln2.eps))
+                        ln=(layer.ln2.weight, layer.ln2.bias, layer.ln2.eps)) if _LN_FUSE else None
     if f is None:
         f = G.decode_linear(layer.ln2(x2), mlp.fc1.weight, mlp.fc1.bias, G.GV_GELU)
     out = G.decode_linear(f, mlp.fc2.weight, mlp.fc2.bias, G.GV_RES, res=x2)

@@ -35,7 +35,8 @@ def test_decode_gemv_epilogues(dtype, M, N, K, epi):
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 8192, 2048), (1, 6144, 2048), (1, 12288, 4096),
-                                   (1, 1000, 1024), (1, 3072, 2048), (4, 4096, 4096)])
+                                   (3, 1000, 1024), (4, 3072, 2048), (4, 4096, 4096), (8, 3072, 2048),
+                                   (16, 6144, 2048), (16, 4096, 4096)])
 @pytest.mark.parametrize("epi", [1, 3])
 def test_decode_gemv_fused_layernorm(M, N, K, epi):
     """LayerNorm fused as the GEMV prologue (LN1 -> QKV, LN2 -> FFN1) vs fp32
@@ -51,7 +52,7 @@ def test_decode_gemv_fused_layernorm(M, N, K, epi):
     lb = (0.1 * torch.randn(K, device=DEV, generator=g)).bfloat16()
     xn = torch.nn.functional.layer_norm(x.float(), (K,), lw.float(), lb.float(), 1e-5)
     ref = xn.bfloat16().float() @ w.float().t() + b.float()
-    if M > 1 or M * K * 2 > 96 * 1024:  # not covered by the fused prologue: caller falls back
+    if M > 4 or M * (K + 8) * 2 > 96 * 1024:  # not covered by the fused prologue: caller falls back
         if epi == G.GV_GELU:
             assert G.decode_linear(x, w, b, epi, ln=(lw, lb, 1e-5)) is None
         return
