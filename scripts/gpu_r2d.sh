@@ -9,5 +9,5 @@ for m in gpt3-6.7B gpt3-1.3B gpt-345M; do
 done
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 3 --warmup 2 > $OUT/prof.log 2>&1 || { echo "prof failed"; tail -5 $OUT/prof.log; exit 1; }
 f=$(find $OUT/prof -name "*kernel_trace.csv" | head -1)
-python3 tools/kernel_summary.py "$f" --window adamw_flat:2:5 --steps 3 --top 32 --md $OUT/kernels_6.7B.md > /dev/null 2>&1
+python3 tools/kernel_summary.py "$f" --window adamw_flat:132:330 --steps 3 --top 32 --md $OUT/kernels_6.7B.md > /dev/null 2>&1
 head -34 $OUT/kernels_6.7B.md
