@@ -235,6 +235,7 @@ struct AttnParams {
   uint32_t klo, khi, thr;
   float drop_scale;
   int dval;              // valid head dim (<= the tile's D; columns past it are zero)
+  int delta_in_dq;       // backward: the dQ pass computes and stores delta (no pre-pass)
   const uint64_t* salt;  // graph mode: per-replay device salt (fx_set_dropout_salt)
 };
 
@@ -555,7 +556,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
     }
   }
   const float lse2 = qvalid ? P.lse[(long)bh * P.Sq + qi] * LOG2E : INFINITY;
-  const float dlt = qvalid ? P.delta[(long)bh * P.Sq + qi] : 0.f;
+  float dlt = 0.f;  // delta = rowsum(dO . O), below (after the first tile's DMA is issued)
   const float sl2 = P.scale * LOG2E;
   const uint32_t cb = DROP ? attn_cb(P, bh) : 0u;
 
@@ -575,6 +576,29 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
   if (ntiles > 0) {
     kld.load(0, smem, lane);
     vld.load(0, smem + 2 * TB, lane);
+  }
+  // delta = rowsum(dO . O): taken here from the dO fragments already in
+  // registers plus one load of the O row (in flight with the first K/V tile) (the dK/dV pass, launched after this
+  // one, reads the stored value), or from the separate pre-pass
+  if (P.delta_in_dq) {
+    float part = 0.f;
+    if (qvalid) {
+      const uint16_t* orow = P.o + b * P.so_b + hd * P.so_h + (long)qi * P.so_s;
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        if (16 * s + 8 * h >= P.dval) continue;
+        float ov[8], gv[8];
+        load8<T>(orow + 16 * s + 8 * h, ov);
+        unpack8<T>(__builtin_bit_cast(uint4, gf[s]), gv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) part += ov[j] * gv[j];
+      }
+    }
+    part += __shfl_xor(part, 32, 64);
+    dlt = qvalid ? part : 0.f;
+    if (qvalid && h == 0) P.delta[(long)bh * P.Sq + qi] = dlt;
+  } else {
+    dlt = qvalid ? P.delta[(long)bh * P.Sq + qi] : 0.f;
   }
   glds_wait();
   __syncthreads();
@@ -1022,7 +1046,12 @@ static int flash_bwd_t(const void* q, const void* k, const void* v, const void* 
   P.so_b = os[0]; P.so_s = os[1]; P.so_h = os[2];
   P.sdk_b = dks[0]; P.sdk_s = dks[1]; P.sdk_h = dks[2];
   P.sdq_b = dqs[0]; P.sdq_s = dqs[1]; P.sdq_h = dqs[2];
-  {
+  static const bool delta_fused = [] {
+    const char* e = getenv("FLEETX_FA_DELTA_IN_DQ");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  P.delta_in_dq = delta_fused ? 1 : 0;
+  if (!delta_fused) {
     const long rows = (long)B * H * Sq;
     const int rpb = 256 / (D / 8 <= 8 ? 8 : 16);  // rows per block (fa_bwd_pre_kernel TPR)
     const int grid = (int)((rows + rpb - 1) / rpb);
