@@ -11,8 +11,9 @@ a representation layer, truncated-normal position embedding.
 embedding for fine-tuning at another resolution.
 
 MI355X mapping: the patch embed is an unfold + GEMM (no conv), attention uses
-the fused non-causal flash kernel (head dims 64 / 96 / 128, other dims such as
-ViT-g's 88 zero-padded to the 96 tile), LN and bias+GeLU(erf) are HIP kernels.
+the fused non-causal flash kernel through the packed [B, N, 3, H, D] QKV entry
+(ViT-g's head dim 88 runs on the 96-wide tile with zero-read columns), LN and
+bias+GeLU(erf) are HIP kernels.
 """
 import math
 import os
