@@ -366,7 +366,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
       vld.load((it + 1) * KV, smem + 2 * TB + (cur ^ 1) * TB, lane);
     }
     const int kb = it * KV;
-    if (!(CAUSAL && kb > wq0 + 31)) {
+    // waves without a valid query (the tail block of S = 257) only help load
+    if (wq0 < P.Sq && !(CAUSAL && kb > wq0 + 31)) {
       floatx16 sacc[2];
       // all K fragments of the tile up front: the 16 LDS reads overlap each
       // other instead of one exposed LDS latency per MFMA
@@ -613,7 +614,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
       vld.load((it + 1) * KV, smem + 2 * TB + (cur ^ 1) * TB, lane);
     }
     const int kb = it * KV;
-    if (!(CAUSAL && kb > wq0 + 31)) {
+    // waves without a valid query (the tail block of S = 257) only help load
+    if (wq0 < P.Sq && !(CAUSAL && kb > wq0 + 31)) {
       const bool need_mask = (CAUSAL && kb + KV - 1 > wq0) || (kb + KV > kv_len);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -802,7 +804,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
     const char* gt = cur + TB;
     const float* lse_s = reinterpret_cast<const float*>(cur + 2 * TB);
     const float* dl_s = lse_s + QT;
-    if (!(CAUSAL && qb + QT - 1 < wk0)) {  // else: whole tile above this wave's keys
+    // else: whole tile above this wave's keys, or the wave holds no valid key
+    if (wk0 < P.Sk && !(CAUSAL && qb + QT - 1 < wk0)) {
 #pragma unroll
       for (int t = 0; t < QT / 32; ++t) {
         const int q0 = qb + 32 * t;
