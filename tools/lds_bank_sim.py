@@ -85,7 +85,48 @@ def search(D):
     return None
 
 
+def loff_subtiled(D):
+    """The kernels' LDS image (csrc/kernels/flash_attn.hip ``loff``): 8-row x
+    32-column subtiles of 512 B with the chunk XORed inside its 4-chunk group."""
+    def off(row, ch):
+        return (16 * D) * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + \
+            16 * ((ch & 3) ^ ((row >> 2) & 3))
+    return off
+
+
+def check_frag():
+    """``Frag`` (flash_attn.hip) reads every operand fragment as a per-lane base
+    plus an immediate; check those closed forms against ``loff`` for every lane,
+    32-row block, k-step and transposed-read block, for D = 64 / 96 / 128."""
+    for D in (64, 96, 128):
+        off = loff_subtiled(D)
+        for lane in range(64):
+            h, r = lane >> 5, lane & 31
+            rbase = 16 * D * (r >> 3) + 64 * (r & 7)
+            rb = [rbase + 16 * (h ^ ((r >> 2) & 3)), rbase + 16 * ((2 + h) ^ ((r >> 2) & 3))]
+            gi, q, p = (lane >> 4) & 1, (lane >> 2) & 3, lane & 3
+            tbase = 64 * (4 * h + q) + 8 * (p & 1)
+            c = 2 * gi + (p >> 1)
+            tb = [tbase + 16 * (c ^ h), tbase + 16 * (c ^ (2 + h)) + 16 * D]
+            for t in range(4):
+                for s in range(D // 16):
+                    assert off(32 * t + r, 2 * s + h) == rb[s & 1] + 64 * D * t + 512 * (s >> 1)
+                for ss in range(2):
+                    for dt in range(D // 32):
+                        kb = 32 * t + 16 * ss + 4 * h
+                        ch = 4 * dt + 2 * gi + (p >> 1)
+                        for e in (0, 1):
+                            want = off(kb + 8 * e + q, ch) + 8 * (p & 1)
+                            assert want == tb[e] + 64 * D * t + 32 * D * ss + 512 * dt
+        print("D=%d: Frag closed forms match loff for all lanes; banks (row, tr) = %s"
+              % (D, test(D, off)))
+
+
 if __name__ == "__main__":
+    import sys
+    if "--check-frag" in sys.argv:
+        check_frag()
+        sys.exit(0)
     for D in (64, 128):
         print("D=%d naive" % D, test(D, make_off(D, (0,) * ((D // 8).bit_length() - 1))))
         print("D=%d found" % D, search(D))
