@@ -221,9 +221,11 @@ class EagerEngine(BasicEngine):
             self._cuda_graph = bool(e.get("cuda_graph", False)) and self._graph_ok(comm)
             self._graph = None
             self._graph_calls = 0
-            # step N's AdamW runs on a side stream under step N+1's forward
+            # step N's AdamW runs on a side stream under step N+1's forward (also
+            # with the fp16 loss scaler: its found-inf / scale live on the device
+            # and the next step() joins the side stream before rewriting them)
             if comm.get("overlap_optimizer", True) and not self._pipeline and not self._cuda_graph \
-                    and self.scaler is None and hasattr(self.optimizer, "enable_forward_overlap"):
+                    and hasattr(self.optimizer, "enable_forward_overlap"):
                 self.optimizer.overlap_grid = int(comm.get("overlap_optimizer_grid", 128))
                 self.optimizer.enable_forward_overlap(model)
             # single data rank: gradient sum-of-squares per bucket under backward
