@@ -88,7 +88,7 @@ int fx_comm_ipc_handle(void*, char*);
 void* fx_comm_ipc_open(const char*);
 int fx_comm_ipc_close(void*);
 int fx_comm_allreduce(int, int, const void*, void*, long, int, int, const uint64_t*, unsigned int*,
-                      unsigned int*, long, hipStream_t);
+                      unsigned int*, long, unsigned long long, hipStream_t);
 }
 
 #define P(x) reinterpret_cast<void*>(x)
@@ -290,11 +290,12 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.def("comm_ipc_close", [](ptr p) { return fx_comm_ipc_close(P(p)); });
   m.def("comm_allreduce", [](int dt, int op, ptr in, ptr out, long n, int rank, int world,
-                             std::vector<uint64_t> peers, ptr epochs, ptr err, long slot, ptr st) {
+                             std::vector<uint64_t> peers, ptr epochs, ptr err, long slot,
+                             unsigned long long timeout_ticks, ptr st) {
     if ((int)peers.size() != world) throw std::runtime_error("need one receive base per rank");
     return fx_comm_allreduce(dt, op, CP(in), P(out), n, rank, world, peers.data(),
                              reinterpret_cast<unsigned int*>(epochs),
-                             reinterpret_cast<unsigned int*>(err), slot, S(st));
+                             reinterpret_cast<unsigned int*>(err), slot, timeout_ticks, S(st));
   });
   m.def("softmax_bwd", [](int dt, ptr y, ptr dy, ptr dx, long rows, int Sq, int Sk, float scale,
                           int causal, ptr st) {

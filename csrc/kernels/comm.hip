@@ -23,8 +23,15 @@
 //    is never overwritten while a peer still reads it;
 //  * reduction runs in rank order 0..world-1 on every rank, so all ranks get
 //    bitwise-identical results (tensor-parallel replicas stay in lock-step);
-//  * every spin is bounded (~2 s of s_memrealtime); a timeout sets *err and
-//    the call completes with garbage instead of hanging the GPU.
+//  * every spin is bounded (`timeout` ticks of the 100 MHz s_memrealtime
+//    clock, FLEETX_ONESHOT_TIMEOUT_S on the host, default 120 s so a peer's
+//    checkpoint save or data stall does not trip it); a timeout never
+//    produces a normal-looking result: the affected outputs are written as
+//    NaN (so the loss / found-inf / NaN guard see it on the next step) and
+//    *err is set, which the engine reads at every logging sync and raises.
+//    The protocol itself survives a timeout: the late peer still finds this
+//    rank's pushed granules of that call, and the next call uses the other
+//    parity, so only the timed-out call's output is lost.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -92,7 +99,7 @@ struct Pack<f16> : Pack16<f16> {};
 template <typename T, int OP>  // OP 0 = sum, 1 = max
 __global__ __launch_bounds__(FX_COMM_THREADS) void ll_allreduce_kernel(
     const T* in, T* out, long n, int rank, int world, PeerTable pt, unsigned int* epochs,
-    unsigned int* err, long slot) {
+    unsigned int* err, long slot, unsigned long long timeout) {
   __shared__ unsigned int s_epoch;
   const int b = blockIdx.x;
   if (threadIdx.x == 0) s_epoch = epochs[b] + 1u;
@@ -117,6 +124,7 @@ __global__ __launch_bounds__(FX_COMM_THREADS) void ll_allreduce_kernel(
   bool timed_out = false;
   for (long g = g0 + threadIdx.x; g < g1; g += blockDim.x) {
     float acc[2] = {0.f, 0.f};
+    bool lost = false;
     for (int p = 0; p < world; ++p) {
       uint32_t w;
       if (p == rank) {
@@ -129,12 +137,13 @@ __global__ __launch_bounds__(FX_COMM_THREADS) void ll_allreduce_kernel(
           do {
             __builtin_amdgcn_s_sleep(1);
             x = get_granule(src);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // ~2 s at 100 MHz
+            if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
               timed_out = true;
               break;
             }
           } while ((x >> 32) != e);
         }
+        if ((x >> 32) != e) lost = true;
         w = (uint32_t)x;
       }
       float v[2];
@@ -150,6 +159,7 @@ __global__ __launch_bounds__(FX_COMM_THREADS) void ll_allreduce_kernel(
         acc[1] = fmaxf(acc[1], v[1]);
       }
     }
+    if (lost) acc[0] = acc[1] = __builtin_nanf("");
     Pack<T>::store(out, g, n, acc);
   }
   if (timed_out)
@@ -160,9 +170,10 @@ __global__ __launch_bounds__(FX_COMM_THREADS) void ll_allreduce_kernel(
 
 template <typename T, int OP>
 void launch(const void* in, void* out, long n, int rank, int world, const PeerTable& pt,
-            unsigned int* epochs, unsigned int* err, long slot, int blocks, hipStream_t s) {
+            unsigned int* epochs, unsigned int* err, long slot, unsigned long long timeout,
+            int blocks, hipStream_t s) {
   hipLaunchKernelGGL((ll_allreduce_kernel<T, OP>), dim3(blocks), dim3(FX_COMM_THREADS), 0, s,
-                     (const T*)in, (T*)out, n, rank, world, pt, epochs, err, slot);
+                     (const T*)in, (T*)out, n, rank, world, pt, epochs, err, slot, timeout);
 }
 
 }  // namespace
@@ -205,10 +216,11 @@ void* fx_comm_ipc_open(const char* in64) {
 int fx_comm_ipc_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
 
 // dt: 0 bf16, 1 fp16, 2 fp32; op: 0 sum, 1 max.  `peers[world]` are the
-// receive bases (own at [rank]); returns the number of blocks launched.
+// receive bases (own at [rank]); `timeout_ticks` bounds every wait for a
+// peer granule (100 MHz ticks); returns the number of blocks launched.
 int fx_comm_allreduce(int dt, int op, const void* in, void* out, long n, int rank, int world,
                       const uint64_t* peers, unsigned int* epochs, unsigned int* err,
-                      long slot_granules, hipStream_t s) {
+                      long slot_granules, unsigned long long timeout_ticks, hipStream_t s) {
   PeerTable pt;
   for (int i = 0; i < FX_COMM_MAX_WORLD; ++i)
     pt.recv[i] = i < world ? reinterpret_cast<unsigned long long*>(peers[i]) : nullptr;
@@ -218,8 +230,8 @@ int fx_comm_allreduce(int dt, int op, const void* in, void* out, long n, int ran
   // the same parity while a slower peer still polls it).
   const int blocks = FX_COMM_MAX_BLOCKS;
 #define FX_AR(T)                                                                          \
-  (op == 0 ? launch<T, 0>(in, out, n, rank, world, pt, epochs, err, slot_granules, blocks, s) \
-           : launch<T, 1>(in, out, n, rank, world, pt, epochs, err, slot_granules, blocks, s))
+  (op == 0 ? launch<T, 0>(in, out, n, rank, world, pt, epochs, err, slot_granules, timeout_ticks, blocks, s) \
+           : launch<T, 1>(in, out, n, rank, world, pt, epochs, err, slot_granules, timeout_ticks, blocks, s))
   if (dt == 0) FX_AR(bf16);
   else if (dt == 1) FX_AR(f16);
   else FX_AR(float);

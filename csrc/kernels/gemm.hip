@@ -38,6 +38,7 @@
 #include <type_traits>
 
 #include "fx_common.h"
+#include "gemm_common.h"
 
 typedef short v4s __attribute__((ext_vector_type(4)));
 #define LDS_AS(p) ((__attribute__((address_space(3))) void*)(p))
@@ -54,35 +55,12 @@ typedef short v4s __attribute__((ext_vector_type(4)));
 #define FX_GEMM_STAMP 0
 #endif
 
+// gemm5.hip: the 4-wave kernel with the hand-scheduled K-loop
+int fx_gemm5_launch(int dt, int la, int lb, int epi, const fxg::GemmParams& P, hipStream_t st);
+
 namespace {
 
-enum { LAY_KC = 0, LAY_MC = 1 };
-enum { EPI_STORE = 0, EPI_BIAS_GELU = 1, EPI_DGELU = 2, EPI_F32 = 3, EPI_BIAS_GELU_ERF = 4,
-       EPI_DGELU_ERF = 5 };
-
-constexpr int BM = 256, BN = 256, BK = 64;
-constexpr int PIECE = 16384;            // bytes per staged piece (128 rows x 64 k x 2 B)
-constexpr int TILE_BYTES = 4 * PIECE;   // one K-tile of A and B
-constexpr int SMEM = 2 * TILE_BYTES;    // double buffer: 128 KiB
-
-struct GemmParams {
-  const uint16_t* A;
-  const uint16_t* B;
-  void* C;
-  const uint16_t* bias;
-  uint16_t* aux;
-  long lda, ldb, ldc, ldaux;
-  int M, N, K;
-  int tiles_m, tiles_n;
-  int beta;
-  int gm;  // tiles per M-group of the block order (L2 reuse)
-  unsigned long long* dbg;  // tools/gemm_lab timeline stamps (FX_GEMM_STAMP builds only)
-};
-
-__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
-  const int xcd = bid & 7, pos = bid >> 3, q = nblk >> 3, r = nblk & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
-}
+using namespace fxg;
 
 // piece-local row (0..127) -> row of the 256-wide block tile.  The A pieces
 // hold rows {wr*128 + h*64 + 0..63}, the B pieces cols {wc*64 + h*32 + 0..31}.
@@ -504,9 +482,6 @@ __device__ __forceinline__ void vm_wait(int n) {
 }
 #undef FX_VMW
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, long bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
-}
 
 // B operand of the persistent kernel: piece h holds the CONTIGUOUS tile
 // columns h*128 + [0, 128) (wave wc's quadrant ni = columns ni*128 + wc*32 +
@@ -1238,6 +1213,10 @@ void launch(const GemmParams& P, hipStream_t st) {
   if (g_variant < 0) {
     const char* e = getenv("FLEETX_GEMM_PF");
     g_variant = e ? atoi(e) : 0;
+  }
+  if (g_variant == 5 && P.K >= 2 * BK) {
+    fx_gemm5_launch(std::is_same<T, f16>::value ? 1 : 0, LA, LB, EPI, P, st);
+    return;
   }
   if (g_variant == 4) {
     auto k4 = gemm4_kernel<T, LA, LB, EPI>;

@@ -1,0 +1,41 @@
+// Shared definitions of the gfx950 GEMM kernels (gemm.hip, gemm5.hip).
+#pragma once
+#include <stdint.h>
+
+#include "fx_common.h"
+
+namespace fxg {
+
+enum { LAY_KC = 0, LAY_MC = 1 };
+enum { EPI_STORE = 0, EPI_BIAS_GELU = 1, EPI_DGELU = 2, EPI_F32 = 3, EPI_BIAS_GELU_ERF = 4,
+       EPI_DGELU_ERF = 5 };
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int PIECE = 16384;            // bytes per staged piece (128 rows x 64 k x 2 B)
+constexpr int TILE_BYTES = 4 * PIECE;   // one K-tile of A and B
+constexpr int SMEM = 2 * TILE_BYTES;    // double buffer: 128 KiB
+
+struct GemmParams {
+  const uint16_t* A;
+  const uint16_t* B;
+  void* C;
+  const uint16_t* bias;
+  uint16_t* aux;
+  long lda, ldb, ldc, ldaux;
+  int M, N, K;
+  int tiles_m, tiles_n;
+  int beta;
+  int gm;  // tiles per M-group of the block order (L2 reuse)
+  unsigned long long* dbg;  // tools/gemm_lab timeline stamps (FX_GEMM_STAMP builds only)
+};
+
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  const int xcd = bid & 7, pos = bid >> 3, q = nblk >> 3, r = nblk & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+}  // namespace fxg

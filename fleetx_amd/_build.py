@@ -53,7 +53,7 @@ def build_kernels(verbose=False, jobs=None):
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(OUT, exist_ok=True)
     kdir = os.path.join(CSRC, "kernels")
-    headers = glob.glob(os.path.join(kdir, "*.h"))
+    headers = glob.glob(os.path.join(kdir, "*.h")) + glob.glob(os.path.join(kdir, "*.inc"))
     hips = sorted(glob.glob(os.path.join(kdir, "*.hip")))
     common = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-munsafe-fp-atomics",
               "-Wno-unused-result"]

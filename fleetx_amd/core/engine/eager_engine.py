@@ -33,6 +33,7 @@ import torch.distributed as dist
 from .basic_engine import BasicEngine
 from ...ops import _lib
 from ...optims import build_optimizer, build_lr_scheduler
+from ...parallel import comm as _comm
 from ...parallel import topology as topo
 from ...parallel.grad_buffer import FlatParamGradBuffer
 from ...parallel.rng import get_rng_state_tracker
@@ -239,6 +240,10 @@ class EagerEngine(BasicEngine):
                 self.buffer.enable_param_gather_overlap(model)
             if self._pipeline:
                 model.attach(self)
+            if self.device.type == "cuda":
+                from ...utils.streams import log_inventory
+                log_inventory(self.hcg, self.optimizer, self.buffer,
+                              _lin.WGRAD_STREAM["enabled"])
         self._profiler = self._build_profiler(configs.get("Profiler"))
         self._inference_engine = None
         self.consumed_samples = 0
@@ -417,6 +422,9 @@ class EagerEngine(BasicEngine):
                 break
         if self._profiler:
             self._profiler.stop()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+            _comm.check_all()
         return global_step
 
     def _train_one_epoch(self, epoch, loader, valid_loader, global_step):
@@ -441,6 +449,9 @@ class EagerEngine(BasicEngine):
             if global_step % self._logging_freq == 0:
                 if torch.cuda.is_available():
                     torch.cuda.synchronize()
+                    # a one-shot all-reduce that timed out on a peer wrote NaN
+                    # and flagged it: stop here, naming the group
+                    _comm.check_all()
                 cost = (time.time() - t0) / self._logging_freq
                 lval = self._reduce_log_loss(loss_acc, n_acc)
                 if self._nan_guard != "off" and not np.isfinite(lval):

@@ -147,6 +147,17 @@ def linear_dgrad(dy2, w, act_input=None, act="gelu"):
     return dx
 
 
+def covers_wgrad(dy2, x2):
+    """Whether :func:`linear_wgrad` takes ``dy2^T x2`` (same checks as the
+    kernel: 16-bit token-major operands, tokens a multiple of 64, extents of
+    8)."""
+    if not enabled() or not _ok(dy2, x2) or dy2.dtype != x2.dtype:
+        return False
+    M, N = dy2.shape
+    return M % 64 == 0 and M >= 64 and N % 8 == 0 and x2.shape[1] % 8 == 0 and N >= 8 \
+        and x2.shape[1] >= 8
+
+
 def linear_wgrad(dy2, x2, out32, accumulate):
     """``out32[N,K] (+)= dy2[M,N]^T @ x2[M,K]`` in fp32.  Returns True if done."""
     if not enabled() or not _ok(dy2, x2) or dy2.dtype != x2.dtype:

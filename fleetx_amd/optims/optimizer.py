@@ -194,7 +194,8 @@ class FlatOptimizer:
             if cur_u is not None:
                 groups.setdefault(cur_u, []).append((ri, lo, e))
         self._overlap_groups = [(u, groups[u]) for u in sorted(groups)]  # root (-1) first
-        self._opt_stream = torch.cuda.Stream(device=buf.device)
+        from ..utils.streams import side_stream
+        self._opt_stream = side_stream(buf.device)
         self._unit_events = {}
         self._overlap_hooks = [model.register_forward_pre_hook(self._make_wait(-1))]
         for i, m in enumerate(units):

@@ -77,6 +77,18 @@ def _check(op, group, t, extra=0):
             ranks, rows))
 
 
+def _op_extra(rop):
+    return zlib.crc32(str(rop).encode()) & 0xFFFF if rop is not None else 0
+
+
+def check_call(op, group, t, rop=None):
+    """Fingerprint a collective issued outside ``torch.distributed`` (the
+    one-shot IPC all-reduce of ``parallel/comm.py``) exactly like the wrapped
+    ones, so a rank that routes a call differently is named too."""
+    if _state["enabled"]:
+        _check(op, group, t, _op_extra(rop))
+
+
 def _wrap(op):
     orig = getattr(dist, op)
 
@@ -89,11 +101,7 @@ def _wrap(op):
                     group = a
                     break
         t = _first_tensor(args, kwargs)
-        extra = 0
-        rop = kwargs.get("op")
-        if rop is not None:
-            extra = zlib.crc32(str(rop).encode()) & 0xFFFF
-        _check(op, group, t, extra)
+        _check(op, group, t, _op_extra(kwargs.get("op")))
         return orig(*args, **kwargs)
     wrapped.__wrapped__ = orig
     return wrapped

@@ -14,10 +14,19 @@ payload straight into every peer's receive area (IPC-mapped device memory,
 rank-ordered reduction so every rank gets bitwise-identical results, device
 side epochs so the call can be captured in a HIP graph).
 
+Failure mode: every wait for a peer is bounded (``FLEETX_ONESHOT_TIMEOUT_S``,
+default 120 s, long enough for a peer's checkpoint save or data stall).  A
+timed-out call writes NaN into the outputs it could not reduce and raises the
+device error flag; :func:`check_all` reads the flags (the engine calls it at
+every logging sync and at the end of ``fit``) and raises naming the group, so
+a slow or dead peer can never silently feed garbage into training.
+
 :class:`Communicator` routes each call: the one-shot kernel when the group is
 one node, the dtype/op are supported and the message fits the receive slot;
-``torch.distributed`` (RCCL) otherwise.  It also owns a dedicated HIP stream
-for collectives issued asynchronously (:meth:`Communicator.all_reduce_async`).
+``torch.distributed`` (RCCL) otherwise.  Whether the one-shot path is used is
+decided collectively (all ranks of the group or none), and with the
+collective fingerprint checker enabled its calls are fingerprinted like the
+RCCL ones (``parallel/collective_check.py``).
 """
 import os
 import socket
@@ -29,12 +38,28 @@ from ..ops import _lib
 
 # bytes of payload per rank above which RCCL's bandwidth-optimal algorithms win
 DEFAULT_MAX_BYTES = int(os.environ.get("FLEETX_ONESHOT_MAX_BYTES", str(256 * 1024)))
+# bound on every wait for a peer inside the kernel (seconds)
+DEFAULT_TIMEOUT_S = float(os.environ.get("FLEETX_ONESHOT_TIMEOUT_S", "120"))
+_TICKS_PER_S = 100_000_000  # s_memrealtime runs at 100 MHz
 _DT = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2}
 _OPS = {dist.ReduceOp.SUM: 0, dist.ReduceOp.MAX: 1}
 
 
 def _group_members(group):
     return list(group.ranks) if group is not None else list(range(dist.get_world_size()))
+
+
+class OneShotTimeout(RuntimeError):
+    pass
+
+
+def _agree(ok, pg, device):
+    """True on every rank iff ``ok`` on every rank of the group."""
+    backend = dist.get_backend(pg)
+    dev = device if backend == "nccl" else torch.device("cpu")
+    f = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(f, op=dist.ReduceOp.MIN, group=pg)
+    return bool(int(f.item()))
 
 
 class IpcAllReduce:
@@ -44,10 +69,12 @@ class IpcAllReduce:
     handles with an all-gather) and then issue the same sequence of calls.
     """
 
-    def __init__(self, group=None, max_bytes=DEFAULT_MAX_BYTES, device=None):
+    def __init__(self, group=None, max_bytes=DEFAULT_MAX_BYTES, device=None,
+                 timeout_s=DEFAULT_TIMEOUT_S):
         k = _lib.kernels()
         self.k = k
         self.group = group
+        self.name = "world" if group is None else str(list(group.ranks))
         pg = group.group if group is not None else None
         members = _group_members(group)
         self.world = len(members)
@@ -56,28 +83,46 @@ class IpcAllReduce:
             raise ValueError("one-shot all-reduce supports up to %d ranks" % k.comm_max_world())
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.max_bytes = int(max_bytes)
+        self.timeout_ticks = int(max(timeout_s, 1e-3) * _TICKS_PER_S)
         self.slot = (self.max_bytes + 3) // 4  # granules (4 payload bytes each) per source
-        self.base = k.comm_alloc(self.slot)
-        if not self.base:
-            raise RuntimeError("hipExtMallocWithFlags(uncached) failed")
-        handle = k.comm_ipc_handle(self.base)
+        self.opened = []
+        self.base = 0
+        # Every step below is reached by every rank, whatever failed locally,
+        # and the outcome is agreed on by all of them: one rank falling back to
+        # RCCL while its peers spin in the kernel (or wait in a barrier) would
+        # hang the group.
+        why = None
+        handle = None
+        try:
+            self.base = k.comm_alloc(self.slot)
+            if not self.base:
+                why = "hipExtMallocWithFlags(uncached) failed"
+            else:
+                handle = k.comm_ipc_handle(self.base)
+        except RuntimeError as e:  # hipIpcGetMemHandle refused, ...
+            why = str(e)
         handles = [None] * self.world
         dist.all_gather_object(handles, (socket.gethostname(), handle), group=pg)
-        if len(set(h for h, _ in handles)) != 1:
-            k.comm_free(self.base)
-            raise RuntimeError("one-shot all-reduce needs every rank of the group on one node")
-        self.opened = []
+        if why is None and len(set(h for h, _ in handles)) != 1:
+            why = "one-shot all-reduce needs every rank of the group on one node"
+        if why is None and any(h is None for _, h in handles):
+            why = "a peer could not export its receive area"
         peers = []
-        for r, (_, h) in enumerate(handles):
-            if r == self.rank:
-                peers.append(self.base)
-                continue
-            p = k.comm_ipc_open(h)
-            if not p:
-                self.close()
-                raise RuntimeError("hipIpcOpenMemHandle failed for rank %d" % r)
-            self.opened.append(p)
-            peers.append(p)
+        if why is None:
+            for r, (_, h) in enumerate(handles):
+                if r == self.rank:
+                    peers.append(self.base)
+                    continue
+                p = k.comm_ipc_open(h)
+                if not p:
+                    why = "hipIpcOpenMemHandle failed for rank %d" % r
+                    break
+                self.opened.append(p)
+                peers.append(p)
+        ok = _agree(why is None, pg, self.device)
+        if not ok:
+            self.close()
+            raise RuntimeError(why or "a peer could not set up the one-shot all-reduce")
         self.peers = peers
         self.epochs = torch.zeros(k.comm_max_blocks(), dtype=torch.int32, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
@@ -105,7 +150,7 @@ class IpcAllReduce:
             cur.wait_event(self._last[1])
         self.k.comm_allreduce(_DT[t.dtype], _OPS[op], t.data_ptr(), out.data_ptr(), t.numel(),
                               self.rank, self.world, self.peers, self.epochs.data_ptr(),
-                              self.err.data_ptr(), self.slot, _lib.stream())
+                              self.err.data_ptr(), self.slot, self.timeout_ticks, _lib.stream())
         if not capturing:  # a graph orders its own nodes
             ev = self._last[1] if self._last is not None and self._last[0] == cur \
                 else torch.cuda.Event()
@@ -115,9 +160,13 @@ class IpcAllReduce:
         return out
 
     def check(self):
-        """Raise if any call timed out waiting for a peer (host sync)."""
+        """Raise if any call timed out waiting for a peer (host sync).  The
+        timed-out outputs were written as NaN; the flag stays set."""
         if int(self.err.item()) != 0:
-            raise RuntimeError("one-shot all-reduce timed out waiting for a peer")
+            raise OneShotTimeout(
+                "one-shot all-reduce on group %s timed out waiting for a peer (> %.1f s; "
+                "FLEETX_ONESHOT_TIMEOUT_S); the affected outputs were written as NaN"
+                % (self.name, self.timeout_ticks / _TICKS_PER_S))
 
     def close(self):
         for p in getattr(self, "opened", []):
@@ -129,19 +178,17 @@ class IpcAllReduce:
 
 
 class Communicator:
-    """Collective front end of one process group (``topology.CommGroup``).
-
-    * ``all_reduce``: one-shot IPC kernel for small single-node messages,
-      RCCL otherwise (``FLEETX_ONESHOT=0`` disables the kernel);
-    * ``all_reduce_async``: the same on this communicator's own HIP stream,
-      ordered after the caller's stream, returning an event to wait on.
-    """
+    """Collective front end of one process group (``topology.CommGroup``):
+    ``all_reduce`` takes the one-shot IPC kernel for small single-node
+    messages and RCCL otherwise (``FLEETX_ONESHOT=0`` disables the kernel).
+    Calls run on the caller's stream (no communicator stream of its own: the
+    per-rank stream budget is fixed by ``GPU_MAX_HW_QUEUES``, see
+    ``utils/streams.py``)."""
 
     def __init__(self, group, max_bytes=DEFAULT_MAX_BYTES, oneshot=None):
         self.group = group
         self.nranks = 1 if group is None else group.nranks
         self.oneshot = None
-        self._stream = None
         if oneshot is None:
             oneshot = os.environ.get("FLEETX_ONESHOT", "1") == "1"
         # FLEETX_ONESHOT_FORCE=1 also enables it over gloo (GPU tests that put
@@ -156,31 +203,20 @@ class Communicator:
                 logger.warning("one-shot all-reduce disabled for %s: %s" % (group, e))
                 self.oneshot = None
 
-    @property
-    def stream(self):
-        if self._stream is None:
-            self._stream = torch.cuda.Stream()
-        return self._stream
-
     def all_reduce(self, t, op=dist.ReduceOp.SUM):
         if self.nranks == 1:
             return t
+        pg = self.group.group if self.group is not None else None
         if self.oneshot is not None and self.oneshot.supports(t, op):
+            from . import collective_check
+            collective_check.check_call("all_reduce", pg, t, op)
             return self.oneshot.all_reduce(t, op)
-        dist.all_reduce(t, op=op, group=self.group.group if self.group is not None else None)
+        dist.all_reduce(t, op=op, group=pg)
         return t
 
-    def all_reduce_async(self, t, op=dist.ReduceOp.SUM):
-        """Issue on the communicator stream; returns an event recorded after it."""
-        cur = torch.cuda.current_stream()
-        s = self.stream
-        s.wait_stream(cur)
-        with torch.cuda.stream(s):
-            self.all_reduce(t, op)
-            ev = torch.cuda.Event()
-            ev.record(s)
-        t.record_stream(s)
-        return ev
+    def check(self):
+        if self.oneshot is not None:
+            self.oneshot.check()
 
 
 _COMMS = {}
@@ -195,6 +231,13 @@ def get_communicator(group):
         c = Communicator(group)
         _COMMS[key] = c
     return c
+
+
+def check_all():
+    """Raise :class:`OneShotTimeout` if any one-shot call of this process timed
+    out (one device read per communicator; call at host syncs)."""
+    for c in _COMMS.values():
+        c.check()
 
 
 def reset():

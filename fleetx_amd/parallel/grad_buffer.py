@@ -248,7 +248,8 @@ class FlatParamGradBuffer:
             return False
         if self.mp_group is not None and any(c.seq_parallel for c in self.categories):
             return False  # finish() all-reduces those grads over mp after the buckets
-        self._norm_stream = torch.cuda.Stream(device=self.device)
+        from ..utils.streams import side_stream
+        self._norm_stream = side_stream(self.device)
         self._norm_part = torch.zeros(len(self.buckets), dtype=torch.float32, device=self.device)
         self._bucket_index = {id(b): i for i, b in enumerate(self.buckets)}
         cat_of = []

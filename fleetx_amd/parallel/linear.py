@@ -79,14 +79,13 @@ def _tn_operands(dy2, x2, colsum=None):
     return transpose2d(dy2, colsum=colsum), transpose2d(x2).t()
 
 
-# Weight-gradient GEMMs on a side stream (Distributed.comm.wgrad_stream, opt-in):
-# the data-gradient chain of backward never waits for them, so on models whose
-# GEMMs under-fill the 256 CUs (hidden <= 2048: 8192 x 1024 x 1024 is 128
-# tiles of 256 x 256) the wgrad of layer l runs beside the dgrad of layer l-1
-# (+1.5 % on 345M / 1.3B).  Joined by the gradient buffer before any collective
-# / the optimizer.  Off by default: two concurrent library GEMMs can both be
-# stream-K kernels whose resident workgroups spin on tiles the other kernel's
-# workgroups keep from being scheduled -- a GPU deadlock, observed on ViT-g.
+# Weight-gradient GEMMs on the shared side stream (Distributed.comm.wgrad_stream,
+# opt-in): the data-gradient chain of backward never waits for them, so on
+# models whose GEMMs under-fill the 256 CUs (hidden <= 2048: 8192 x 1024 x 1024
+# is 128 tiles of 256 x 256) the wgrad of layer l runs beside the dgrad of
+# layer l-1 (+1.5 % on 345M / 1.3B).  Joined by the gradient buffer before any
+# collective / the optimizer.  Only wgrads on the hand-written kernel go there
+# (see accumulate_wgrad): two concurrent vendor stream-K GEMMs can deadlock.
 WGRAD_STREAM = {"enabled": False, "stream": None}
 
 
@@ -95,7 +94,8 @@ def _wgrad_side_stream(dev):
         return None
     s = WGRAD_STREAM["stream"]
     if s is None or s.device != dev:
-        s = torch.cuda.Stream(device=dev)
+        from ..utils.streams import side_stream
+        s = side_stream(dev)
         WGRAD_STREAM["stream"] = s
     return s
 
@@ -114,8 +114,17 @@ def accumulate_wgrad(weight, dy2, x2, bias=None, notify=True):
     With ``bias`` (a Parameter) the bias gradient ``sum_rows(dy2)`` is produced
     too: straight into ``bias.main_grad`` when the bias takes fused grads
     (returns None), else returned as a tensor for autograd."""
-    side = _wgrad_side_stream(dy2.device) if dy2.is_cuda and (bias is None or _fused(bias)) \
-        else None
+    # Side stream only (a) for weights with ONE gradient part: a tied weight
+    # (word embedding: LM-head wgrad + lookup backward) has its other part
+    # accumulated into the same main_grad on the main stream; and (b) when
+    # the GEMM runs on the hand-written kernel: two vendor stream-K GEMMs in
+    # flight on two streams can deadlock (workgroups of one spin on tiles the
+    # other's resident workgroups keep from being scheduled; seen on ViT-g)
+    side = None
+    if dy2.is_cuda and (bias is None or _fused(bias)) and \
+            getattr(weight, "_fx_grad_parts", 1) == 1 and G.use("wgrad", dy2, x2) and \
+            G.covers_wgrad(dy2, x2):
+        side = _wgrad_side_stream(dy2.device)
     if side is None:
         return _accumulate_wgrad(weight, dy2, x2, bias, notify)
     side.wait_stream(torch.cuda.current_stream())

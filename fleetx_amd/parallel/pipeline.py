@@ -10,12 +10,13 @@ the loss (averaged over micro-batches) and the tied embedding grad is reduced
 between the first and last stage.
 
 MI355X design:
-* two RCCL communicators per pipe group, one per DIRECTION: activations
-  (stage s -> s+1, and the ring edge of the interleaved schedule) on the
-  forward communicator, gradients (s+1 -> s) on the backward one.  Each
-  direction is its own in-order stream of grouped ``batch_isend_irecv``
-  calls (``ncclGroupStart/End``), so a gradient never queues behind an
-  activation and both directions of the xGMI link run at once;
+* grouped ``batch_isend_irecv`` calls (``ncclGroupStart/End``) on one RCCL
+  communicator per pipe group by default -- an in-order stream that is
+  deadlock-free whatever hardware queue it lands in; with
+  ``Distributed.comm.pp_split_directions`` activations (stage s -> s+1, and
+  the ring edge of the interleaved schedule) and gradients (s+1 -> s) get a
+  communicator each, so a gradient never queues behind an activation (needs
+  ``GPU_MAX_HW_QUEUES`` >= the peer-waiting streams, ``utils/streams.py``);
 * nothing waits for a SEND: the compute stream only waits for a receive, and
   only where the received tensor is consumed (``_Recv.wait``).  Posting the
   receive of the next micro-batch's input together with the current send lets

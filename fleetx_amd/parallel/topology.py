@@ -89,7 +89,7 @@ class HybridTopology:
 class HybridCommunicateGroup:
     """Holds every communicator of the hybrid layout for this rank."""
 
-    def __init__(self, dp=1, mp=1, pp=1, sharding=1):
+    def __init__(self, dp=1, mp=1, pp=1, sharding=1, pp_split_directions=False):
         self.topo = HybridTopology(dp=dp, pp=pp, sharding=sharding, mp=mp)
         self.initialized = dist.is_initialized()
         self.global_rank = dist.get_rank() if self.initialized else 0
@@ -110,11 +110,15 @@ class HybridCommunicateGroup:
         self._groups["check"] = self._build(self._check_groups())
         # first/last pipeline stage pairs for the tied embedding
         self._groups["embedding"] = self._build(self._embedding_groups())
-        # second communicator over each pipe group: backward-direction p2p
-        # (gradients flowing stage s+1 -> s) gets its own RCCL stream, so it
-        # never queues behind forward activations (parallel/pipeline.py)
+        # Optional second communicator over each pipe group
+        # (Distributed.comm.pp_split_directions): backward-direction p2p gets
+        # its own RCCL stream.  Off by default: with more peer-waiting streams
+        # than GPU_MAX_HW_QUEUES two directions can land in one in-order
+        # hardware queue in opposite orders on neighbouring stages
+        # (utils/streams.py); one communicator is deadlock-free whatever the
+        # mapping.
         self._groups["pipe_bwd"] = self._build(self.topo.axis_groups("pipe")) \
-            if pp > 1 else self._groups["pipe"]
+            if pp > 1 and pp_split_directions else self._groups["pipe"]
 
     def _build(self, rank_lists):
         mine = None
@@ -231,9 +235,10 @@ def _want_gloo():
     return os.environ.get("FLEETX_GLOO_SIDE_GROUPS", "0") == "1"
 
 
-def init_hcg(dp=1, mp=1, pp=1, sharding=1):
+def init_hcg(dp=1, mp=1, pp=1, sharding=1, pp_split_directions=False):
     global _HCG
-    _HCG = HybridCommunicateGroup(dp=dp, mp=mp, pp=pp, sharding=sharding)
+    _HCG = HybridCommunicateGroup(dp=dp, mp=mp, pp=pp, sharding=sharding,
+                                  pp_split_directions=pp_split_directions)
     return _HCG
 
 

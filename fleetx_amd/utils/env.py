@@ -40,8 +40,10 @@ def init_dist_env(config, backend=None):
         os.environ.setdefault("TORCH_DISTRIBUTED_DEBUG", "INFO")
     _check_env(config)
     topo.init_distributed(backend=backend, timeout_s=int(d.get("timeout_s", 1800) or 1800))
+    comm = d.get("comm", {}) or {}
     hcg = topo.init_hcg(dp=d.dp_degree, mp=d.mp_degree, pp=d.pp_degree,
-                        sharding=d.sharding.sharding_degree)
+                        sharding=d.sharding.sharding_degree,
+                        pp_split_directions=bool(comm.get("pp_split_directions", False)))
     if dbg == "fingerprint":
         # per-collective op / sequence / shape / dtype cross-check over gloo
         # mirrors of every group (parallel/collective_check.py)

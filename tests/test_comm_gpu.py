@@ -87,3 +87,44 @@ def test_oneshot_allreduce_two_ranks_one_gpu():
                 assert e <= tol, (dt, e)
     # all ranks see bitwise-identical results
     assert res[0][0] == res[1][0]
+
+
+def _late_peer(rank, world):
+    """Rank 1 calls 2 s after rank 0 with a 0.5 s timeout: rank 0's call must
+    come back as NaN with the error flag raised (never a normal-looking
+    result), rank 1's call completes correctly, and the next call of both
+    ranks is correct again (the protocol survives a timeout)."""
+    import time
+    import torch.distributed as dist
+    from fleetx_amd.parallel.comm import IpcAllReduce, OneShotTimeout
+    torch.cuda.set_device(0)
+    ar = IpcAllReduce(None, max_bytes=16 * 1024, timeout_s=0.5)
+    x = torch.full((1000,), float(rank + 1), device="cuda")
+    dist.barrier()
+    if rank == 1:
+        time.sleep(2.0)
+    y = ar.all_reduce(x.clone())
+    torch.cuda.synchronize()
+    first = y.cpu()
+    raised = False
+    try:
+        ar.check()
+    except OneShotTimeout as e:
+        raised = "timed out" in str(e)
+    dist.barrier()
+    z = ar.all_reduce(torch.full((1000,), float(10 * (rank + 1)), device="cuda"))
+    torch.cuda.synchronize()
+    second = z.cpu()
+    dist.barrier()
+    ar.close()
+    return bool(torch.isnan(first).all()), bool((first == 3.0).all()), raised, \
+        bool((second == 30.0).all())
+
+
+def test_oneshot_timeout_poisons_and_raises():
+    res = dist_utils.run(_late_peer, 2, timeout=300)
+    nan0, ok0, raised0, next0 = res[0]
+    nan1, ok1, raised1, next1 = res[1]
+    assert nan0 and raised0, res[0]          # the waiting rank: NaN + flag
+    assert ok1 and not raised1, res[1]       # the late rank found rank 0's data
+    assert next0 and next1                   # the following call is correct on both

@@ -41,3 +41,50 @@ def test_decode_split_rule():
     assert decode_splits(1, 16, 192) == 1          # short context: one split, no combine
     assert decode_splits(1, 32, 32768) == 64       # long context fills the chip
     assert decode_splits(64, 32, 32768) == 1       # enough (b, h) pairs already
+
+
+def test_engine_raises_on_oneshot_timeout(monkeypatch):
+    """fit() reads the one-shot error flags at every logging sync and stops,
+    instead of training on NaN-poisoned all-reduce outputs."""
+    import pytest
+    from fleetx_amd.parallel import comm
+    from fleetx_amd.core.engine import eager_engine
+
+    calls = []
+
+    def boom():
+        calls.append(1)
+        raise comm.OneShotTimeout("one-shot all-reduce on group [0, 1] timed out")
+
+    monkeypatch.setattr(comm, "check_all", boom)
+    monkeypatch.setattr(eager_engine.torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(eager_engine.torch.cuda, "synchronize", lambda *a, **k: None)
+    eng = eager_engine.EagerEngine.__new__(eager_engine.EagerEngine)
+    eng._logging_freq = 1
+    eng._configs = type("C", (), {"Global": type("G", (), {"global_batch_size": 1})()})()
+    eng._fit_impl = lambda batch: None
+    eng._fault_check = lambda step: None
+    eng.device = eager_engine.torch.device("cpu")
+    eng.consumed_samples = 0
+    with pytest.raises(comm.OneShotTimeout):
+        eng._train_one_epoch(0, [[eager_engine.torch.zeros(1)]], None, 0)
+    assert calls
+
+
+def test_stream_inventory_counts_peer_waiting_streams():
+    from fleetx_amd.utils import streams
+
+    class G:
+        def __init__(self, ranks):
+            self.ranks, self.group = ranks, object()
+
+    class H:
+        _groups = {"model": G([0, 1]), "pipe": None, "data": G([0, 2])}
+
+    h = H()
+    h._groups["pipe_bwd"] = h._groups["model"]   # same communicator: counted once
+    inv = streams.inventory(h)
+    names = [n for n, _ in inv]
+    assert names[0] == "compute"
+    assert sum(1 for n in names if n.startswith("rccl:")) == 2
+    assert all(p for n, p in inv if n.startswith("rccl:"))

@@ -55,6 +55,12 @@ int main(int argc, char** argv) {
     };
     printf("{\"gemm\": \"%s\"", s.name);
     for (auto& c : cases) {
+      const char* only = getenv("LAB_ONLY");  // e.g. "fc1:fwd"
+      if (only) {
+        char want[64];
+        snprintf(want, sizeof(want), "%s:%s", s.name, c.nm);
+        if (strcmp(want, only)) continue;
+      }
       auto run = [&]() {
         int rc = fx_gemm(0, c.la, c.lb, c.epi, c.m, c.n, c.k, c.A, c.lda, c.B, c.ldb, c.C, c.ldc,
                          nullptr, aux, c.n, 1, 0);
