@@ -11,11 +11,16 @@ Config = BASELINE.json metric "tokens/sec (whole node) GPT-3 6.7B
 hybrid-parallel at 1/2/4/8 MI355X": h 4096, 32 layers, 32 heads, vocab
 50304, seq 1024, dropout 0.1 (as ``pretrain_gpt_6.7B_sharding16.yaml``), bf16
 compute with fp32 master weights, synthetic tokens, random-init weights.
-Layouts: chosen per GPU count by the MI355X layout planner
+Layouts: BASELINE.json config 3's hybrid family by default on N > 1 GPUs --
+N=8: TP2 x PP2 x DP2 (1F1B, micro-batch 4, 8 micro-batches per step),
+N=4: TP2 x PP2, N=2: TP2 -- so the scaling curve runs tensor- and
+pipeline-parallel traffic over RCCL/xGMI, not only data parallel; one GPU
+runs the planner's choice (micro-batch 8, no recompute for 6.7B).
+``--layout planner`` asks the MI355X layout planner on N > 1 too
 (``fleetx_amd/parallel/auto/planner.py``: step-time model with per-link xGMI
-bandwidth, 1F1B bubble, ZeRO traffic and the 288 GB budget) unless
-``--layout dp,mp,pp,micro[,sharding[,stage]]`` pins one (e.g. the BASELINE
-TP2*PP2*DP2 config: ``--layout 2,2,2,2``).  Weak scaling: 8 sequences x 1024
+bandwidth, 1F1B bubble, ZeRO traffic and the 288 GB budget), and
+``--layout dp,mp,pp,micro[,sharding[,stage]]`` pins one.  The JSON line's
+``config.parallelism`` names the layout.  Weak scaling: 8 sequences x 1024
 tokens of work per GPU per step.
 """
 import argparse
@@ -48,6 +53,9 @@ PEAK_BF16 = PEAK_DENSE_FLOPS["bfloat16"]  # MI355X dense bf16 (spec), per GPU
 # row 1 (345M single card, 16.2k tokens/s) and row 4 (1.3B dp8, ~3.3k tokens/s/GPU,
 # derived).  The 6.7B headline config has no published reference number.
 REF_TOKENS_PER_GPU = {"gpt-345M": 16200.0, "gpt3-1.3B": 3300.0}
+# BASELINE.json config 3 ("GPT-3 6.7B TP=2 PP=2 DP=2 on 8 x MI355X, 1F1B +
+# RCCL") and its sub-node members: dp,mp,pp,micro (per-GPU work fixed)
+CONFIG3_FAMILY = {2: "1,2,1,8", 4: "1,2,2,4", 8: "2,2,2,4"}
 
 
 
@@ -61,7 +69,8 @@ def parse():
     ap.add_argument("--per-gpu-seqs", type=int, default=8,
                     help="sequences of work per GPU per step (weak scaling)")
     ap.add_argument("--layout", default=None,
-                    help="dp,mp,pp,micro[,sharding[,stage]] override, e.g. 2,2,2,2")
+                    help="'planner', or dp,mp,pp,micro[,sharding[,stage]], e.g. 2,2,2,4 "
+                         "(default: BASELINE config-3 family for gpt3-6.7B, planner otherwise)")
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--sequence-parallel", action="store_true")
     ap.add_argument("--no-dropout", action="store_true")
@@ -96,8 +105,11 @@ def main():
     global_batch = args.per_gpu_seqs * n
     recompute = bool(args.recompute)
     sharding, stage = 1, 1
-    if args.layout:
-        vals = [int(x) for x in args.layout.split(",")]
+    layout = args.layout
+    if layout is None and n > 1:
+        layout = CONFIG3_FAMILY.get(n)
+    if layout and layout != "planner":
+        vals = [int(x) for x in layout.split(",")]
         dp, mp, pp, micro = vals[:4]
         sharding = vals[4] if len(vals) > 4 else 1
         stage = vals[5] if len(vals) > 5 else 1
@@ -186,7 +198,8 @@ def main():
     mfu = tps * fpt / (n * PEAK_BF16)
     par = "_".join(x for x in (
         "dp%d" % dp if dp > 1 else "", "sharding%d_stage%d" % (sharding, stage) if sharding > 1
-        else "", "tp%d" % mp if mp > 1 else "", "pp%d" % pp if pp > 1 else "") if x) or "dp1"
+        else "", "tp%d" % mp if mp > 1 else "", "pp%d" % pp if pp > 1 else "",
+        "sp" if args.sequence_parallel and mp > 1 else "") if x) or "dp1"
     if env.get_rank() == 0:
         out = {
             "metric": "tokens/sec (whole node) GPT-3 6.7B hybrid-parallel at 1/2/4/8 MI355X"
@@ -201,6 +214,13 @@ def main():
             "data": "synthetic (random tokens), random-init weights",
             "config": {"model": args.model, "global_batch": global_batch, "seq_len": S,
                        "parallelism": par, "micro_batch": micro,
+                       "layout": {"dp": dp, "tp": mp, "pp": pp, "sharding": sharding,
+                                  "sharding_stage": stage, "micro_batch": micro,
+                                  "accumulate_steps": local_batch // max(micro, 1),
+                                  "schedule": "1F1B" if pp > 1 else "none",
+                                  "source": "cli" if args.layout not in (None, "planner")
+                                  else ("planner" if layout in (None, "planner")
+                                        else "baseline-config3-family")},
                        "hip_graph": bool(getattr(engine, "_cuda_graph", False)),
                        "grad_reduce_dtype": grad_wire,
                        "dropout": drop, "recompute": recompute},

@@ -1205,14 +1205,14 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmParams P) {
   }
 }
 
-static int g_variant = -1;  // FLEETX_GEMM_PF: 0 = plain (default), 1 = prefetching, 2/3 = persistent (prefetching / staggered)
+static int g_variant = -1;  // FLEETX_GEMM_PF: 5 = hand-scheduled 4-wave (gemm5.hip, default; K >= 128), 0 = plain 8-wave, 1 = prefetching, 2/3 = persistent, 4 = 4-wave HIP
 static int g_gm = -1;       // FLEETX_GEMM_GM: M-group height of the tile order (default 8)
 
 template <typename T, int LA, int LB, int EPI>
 void launch(const GemmParams& P, hipStream_t st) {
   if (g_variant < 0) {
     const char* e = getenv("FLEETX_GEMM_PF");
-    g_variant = e ? atoi(e) : 0;
+    g_variant = e ? atoi(e) : 5;
   }
   if (g_variant == 5 && P.K >= 2 * BK) {
     fx_gemm5_launch(std::is_same<T, f16>::value ? 1 : 0, LA, LB, EPI, P, st);

@@ -25,6 +25,7 @@ import contextlib
 import os
 import sys
 import time
+import weakref
 
 import numpy as np
 import torch
@@ -43,6 +44,19 @@ from ...utils.log import logger
 from ...utils.profiler import phase
 
 _END = object()
+_GRAPH_PTR_OWNER = [None]  # id of the engine whose device salt / lr pointers are registered
+
+
+def _release_graph_ptrs(owner):
+    if _GRAPH_PTR_OWNER[0] != owner:
+        return
+    _GRAPH_PTR_OWNER[0] = None
+    try:
+        k = _lib.kernels()
+        k.set_dropout_salt(0)
+        k.set_adamw_lr_ptr(0)
+    except Exception:  # interpreter shutdown / library gone
+        pass
 
 
 class DynamicLossScaler:
@@ -294,6 +308,11 @@ class EagerEngine(BasicEngine):
         self._graph_lr = torch.zeros(1, dtype=torch.float32, device=self.device)
         k.set_dropout_salt(self._graph_salt.data_ptr())
         k.set_adamw_lr_ptr(self._graph_lr.data_ptr())
+        # the kernels read these process-global device pointers: clear them when
+        # this engine goes away (unless a newer engine has taken them over), so
+        # a later engine / optimizer never reads freed memory
+        _GRAPH_PTR_OWNER[0] = id(self)
+        weakref.finalize(self, _release_graph_ptrs, id(self))
 
     def _graph_body(self, batch):
         """The device work of one step: fresh dropout salt, forward, backward,
@@ -345,7 +364,7 @@ class EagerEngine(BasicEngine):
                 self._graph_loss = self._graph_body(self._graph_static)
             self._graph = g
             g.replay()  # the capture itself does not execute the step
-            loss = self._graph_loss
+            loss = self._graph_loss.clone()
         elif not self._graph_batch_matches(batch):
             # a batch of another shape (e.g. a short last batch): run it eagerly
             # with the same device-side salt / lr; the graph stays for the rest
@@ -356,7 +375,9 @@ class EagerEngine(BasicEngine):
                     dst.copy_(src, non_blocking=True)
             self._graph.replay()
             self.optimizer.step_count += 1  # the captured step() ran its host part once
-            loss = self._graph_loss
+            # the captured loss is one static tensor that every replay rewrites:
+            # hand out a copy (fit() accumulates it across steps)
+            loss = self._graph_loss.clone()
         if self.lr_scheduler is not None and hasattr(self.lr_scheduler, "step"):
             self.lr_scheduler.step()
         return loss

@@ -44,12 +44,42 @@ def set_mode(mode):
     _MODE = mode
 
 
-# GEMM kinds routed to the MFMA kernel under FLEETX_GEMM=auto (kinds where it
-# beats hipBLASLt incl. the transposes hipBLASLt needs; tools/bench_gemm.py)
-# Measured on the 6.7B step (profiles/r2_gemm/): every kind currently costs
-# 8-17 ms/step against hipBLASLt, so none is routed by default.
-AUTO_KINDS = set(k for k in os.environ.get("FLEETX_GEMM_AUTO", "").split(",") if k)
-_AUTO_WGRAD = os.environ.get("FLEETX_GEMM_AUTO_WGRAD", "1") == "1"  # shape-routed wgrad
+# GEMM kinds routed to the MFMA kernel under FLEETX_GEMM=auto.  The
+# hand-scheduled 4-wave kernel (csrc/kernels/gemm5.hip) takes
+#  * wgrad: the fp32-accumulating weight gradient in its native token-major
+#    layout -- 1.23-1.43 PF against 1.01-1.18 PF for hipBLASLt's TN path plus
+#    the two transposes it needs (profiles/r3_gemm/);
+#  * dgrad: the data gradient with the weight read in place (hardware
+#    transposed LDS reads) -- 1.41-1.54 PF against 1.41-1.48 PF for the TN
+#    path with its weight transpose;
+#  * dgrad_act / fwd_act (opt-in): the GEMMs with a fused GeLU' / bias+GeLU
+#    epilogue.  Measured in the 6.7B step they lose: the GeLU math runs with
+#    the matrix pipe idle at one workgroup per CU (0.97 ms vs 0.77 ms for the
+#    plain GEMM on FC2's data gradient, more than the 0.16 ms elementwise
+#    pass they retire), and a forward GEMM that holds whole CUs starves the
+#    forward-overlapped AdamW (profiles/r3_step/);
+# forward GEMMs stay on hipBLASLt, whose TN kernels tie or lead there.
+# Only shapes whose output fills the chip (>= 192 tiles of 256 x 256 on the
+# 256 CUs) go to the kernel; FLEETX_GEMM_AUTO="kind,kind" replaces the set.
+_DEFAULT_AUTO = "wgrad,dgrad"
+AUTO_KINDS = set(k for k in os.environ.get("FLEETX_GEMM_AUTO", _DEFAULT_AUTO).split(",") if k)
+MIN_TILES = int(os.environ.get("FLEETX_GEMM_MIN_TILES", "192"))
+
+
+def _tiles(r, c):
+    return ((r + 255) // 256) * ((c + 255) // 256)
+
+
+def out_tiles(kind, a, b):
+    """256 x 256 output tiles of GEMM ``kind`` on operands (a, b) as passed to
+    :func:`use`: fwd (x, w) -> [M, N]; dgrad (dy, w) -> [M, K]; wgrad (dy, x)
+    -> [N, K]."""
+    M = a.numel() // a.shape[-1]
+    if kind.startswith("fwd"):
+        return _tiles(M, b.shape[0])
+    if kind.startswith("dgrad"):
+        return _tiles(M, b.shape[1])
+    return _tiles(a.shape[-1], b.shape[-1])
 
 
 def use(kind, a, b=None):
@@ -59,26 +89,10 @@ def use(kind, a, b=None):
     if _MODE == "blas" or not a.is_cuda or a.dtype not in (torch.bfloat16, torch.float16):
         return False
     if _MODE == "auto":
-        if kind in AUTO_KINDS:
-            return True
-        if kind == "wgrad" and _AUTO_WGRAD and b is not None:
-            # measured routing (tools/bench_gemm.py, profiles/r2_final/gemm_hidden_sweep.jsonl):
-            # the fp32-accumulating weight-gradient GEMM in the native token-major
-            # layout beats hipBLASLt's TN path plus its two transposes when the
-            # [N, K] output is one to two waves of 256x256 tiles on the 256 CUs
-            # (1.3B QKV/FC1/FC2 +3/+15/+11 % isolated, +0.7 % on the whole 1.3B step);
-            # more tiles favour hipBLASLt, fewer leave CUs idle.  The 6.7B
-            # out-proj (4096 x 4096, +7 % isolated) measured -0.3 % in the step,
-            # so square 4096+ outputs stay on hipBLASLt
-            return wgrad_routed(a.shape[1], b.shape[1])
-        return False
+        if kind not in AUTO_KINDS or b is None:
+            return False
+        return out_tiles(kind, a, b) >= MIN_TILES
     return True
-
-
-def wgrad_routed(N, K):
-    """Whether the auto routing sends a ``[N, K]`` weight gradient to the MFMA kernel."""
-    tiles = (N // 256) * (K // 256)
-    return 192 <= tiles <= 512 and min(N, K) <= 2048
 
 
 def _ok(*ts):

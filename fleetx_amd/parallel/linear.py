@@ -232,16 +232,27 @@ def dgrad_gemm(dy, w, act_input=None, act="gelu", colsum=None):
     """``dy @ w`` (times ``gelu'(act_input)`` when given) on the MFMA kernel.
     ``colsum = (dst_f32, accumulate)``: column sums of the result as well (the
     fallback takes them from the dGeLU pass; the caller reduces otherwise and
-    gets ``done = False`` back through ``colsum_done``)."""
-    if G.use("dgrad" if act_input is None else "dgrad_act", dy, w):
-        dy2 = dy.reshape(-1, dy.shape[-1])
-        ai = None if act_input is None else act_input.reshape(-1, act_input.shape[-1])
+    gets ``done = False`` back through ``colsum_done``).
+
+    With ``act_input`` the GeLU' is fused into the GEMM epilogue only where
+    the routing table says so (``dgrad_act``); otherwise the GEMM runs plain
+    (MFMA kernel or hipBLASLt, ``dgrad``) and the separate dGeLU pass also
+    takes the bias column sums."""
+    dy2 = dy.reshape(-1, dy.shape[-1])
+    if act_input is not None and G.use("dgrad_act", dy, w):
+        ai = act_input.reshape(-1, act_input.shape[-1])
         dx = G.linear_dgrad(dy2, w, act_input=ai, act=act)
         if dx is not None:
             if colsum is not None:
                 colsum_into(dx, colsum[0], colsum[1])
             return dx.view(*dy.shape[:-1], w.shape[1])
-    dx = dgrad(dy, w)
+    dx = None
+    if G.use("dgrad", dy, w):
+        dx = G.linear_dgrad(dy2, w)
+        if dx is not None:
+            dx = dx.view(*dy.shape[:-1], w.shape[1])
+    if dx is None:
+        dx = dgrad(dy, w)
     if act_input is not None:
         from ..ops.elementwise import gelu_grad
         dx = gelu_grad(dx, act_input, erf=(act != "gelu"), colsum=colsum)

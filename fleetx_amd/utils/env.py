@@ -25,6 +25,32 @@ def get_world_size():
     return int(os.environ.get("WORLD_SIZE", "1"))
 
 
+# RCCL settings for the large data-parallel / ZeRO gradient buckets and
+# parameter all-gathers (Distributed.comm.rccl_env overrides; the process
+# environment always wins).  An 8-GPU MI355X node is a fully connected xGMI
+# mesh (7 point-to-point links per GPU): a bandwidth-optimal collective needs
+# enough channels that every link carries one, so the channel floor is
+# raised to 32 (RCCL picks fewer for some sizes).  tools/bench_collectives.py
+# reports bus bandwidth against the per-link rate.
+DEFAULT_RCCL_ENV = {"NCCL_MIN_NCHANNELS": "32"}
+
+
+def apply_rccl_env(config=None):
+    """Export the RCCL environment before the process group is created;
+    returns the settings in effect."""
+    env = dict(DEFAULT_RCCL_ENV)
+    if config is not None:
+        comm = (config.get("Distributed", {}) or {}).get("comm", {}) or {}
+        extra = comm.get("rccl_env", None)
+        if extra is False:  # Distributed.comm.rccl_env: False -> RCCL defaults
+            env = {}
+        elif extra:
+            env.update({str(k): str(v) for k, v in dict(extra).items()})
+    for k, v in env.items():
+        os.environ.setdefault(k, v)
+    return {k: os.environ[k] for k in env}
+
+
 def init_dist_env(config, backend=None):
     """Create the process group and the hybrid topology from ``Distributed``."""
     set_debug_modes(config)
@@ -39,6 +65,8 @@ def init_dist_env(config, backend=None):
     elif dbg == "info":
         os.environ.setdefault("TORCH_DISTRIBUTED_DEBUG", "INFO")
     _check_env(config)
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        apply_rccl_env(config)
     topo.init_distributed(backend=backend, timeout_s=int(d.get("timeout_s", 1800) or 1800))
     comm = d.get("comm", {}) or {}
     hcg = topo.init_hcg(dp=d.dp_degree, mp=d.mp_degree, pp=d.pp_degree,

@@ -25,15 +25,32 @@ def test_communicator_falls_back_to_torch_distributed():
         assert y == [3.0] * 5 and m == 1.0
 
 
-def test_wgrad_routing_table():
-    from fleetx_amd.ops.gemm import wgrad_routed
-    # 1.3B: QKV (6144 x 2048), FC1 (8192 x 2048), FC2 (2048 x 8192) -> MFMA kernel
-    assert wgrad_routed(6144, 2048) and wgrad_routed(8192, 2048) and wgrad_routed(2048, 8192)
-    # 1.3B out-proj (too few tiles), 6.7B shapes, 345M shapes, LM head -> hipBLASLt
-    assert not wgrad_routed(2048, 2048)
-    assert not wgrad_routed(4096, 4096) and not wgrad_routed(16384, 4096)
-    assert not wgrad_routed(1024, 1024) and not wgrad_routed(4096, 1024)
-    assert not wgrad_routed(50304, 2048)
+def test_gemm_routing_table():
+    from types import SimpleNamespace as NS
+    from fleetx_amd.ops import gemm as G
+
+    def t(*shape):  # a shape-only stand-in for a bf16 GPU tensor
+        return NS(shape=shape, numel=lambda: __import__("math").prod(shape), is_cuda=True,
+                  dtype=torch.bfloat16)
+    old = G._MODE
+    try:
+        G.set_mode("auto")
+        x, w_qkv = t(8192, 4096), t(12288, 4096)
+        # 6.7B: weight gradients and the fused-epilogue GEMMs go to the MFMA kernel
+        assert G.out_tiles("wgrad", t(8192, 12288), x) == 48 * 16
+        assert G.use("wgrad", t(8192, 12288), x) and G.use("wgrad", t(8192, 4096), x)
+        assert not G.use("fwd_act", x, t(16384, 4096))          # opt-in (FLEETX_GEMM_AUTO)
+        assert G.use("dgrad", t(8192, 12288), w_qkv)
+        # plain forward GEMMs stay on hipBLASLt
+        assert not G.use("fwd", x, w_qkv)
+        # 1.3B out-proj wgrad (64 tiles) and 345M shapes under-fill the chip
+        assert not G.use("wgrad", t(8192, 2048), t(8192, 2048))
+        assert not G.use("wgrad", t(8192, 1024), t(8192, 1024))
+        assert G.use("wgrad", t(8192, 6144), t(8192, 2048))       # 1.3B qkv: 192 tiles
+        G.set_mode("blas")
+        assert not G.use("wgrad", t(8192, 12288), x)
+    finally:
+        G.set_mode(old)
 
 
 def test_decode_split_rule():

@@ -6,7 +6,8 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-SHAPES = [(256, 256, 64), (512, 768, 1024), (296, 520, 192), (1024, 1000, 320), (64, 256, 128)]
+SHAPES = [(256, 256, 64), (512, 768, 1024), (296, 520, 192), (1024, 1000, 320), (64, 256, 128),
+          (384, 260, 256)]  # N % 8 == 4: the direct (unstaged) epilogue
 
 
 def _rel(out, ref):
@@ -29,8 +30,10 @@ def gemm():
     from fleetx_amd.ops import gemm as G
     from fleetx_amd.ops import _lib
     _lib.kernels()
+    old = G._MODE
     G.set_mode("hip")
-    return G
+    yield G
+    G.set_mode(old)  # later modules pick their GEMM routing on purpose
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])

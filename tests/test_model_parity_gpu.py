@@ -5,6 +5,13 @@ copied weights, dropout off.  Logits, loss and every parameter gradient are
 compared with relative-error bounds.
 
 GPT: reference ``gpt/dygraph/single_model.py`` (pre-LN decoder, tied LM head).
+
+Every test runs twice, with the GEMMs forced onto the hand-written MFMA
+kernels (``FLEETX_GEMM=hip``) and with the default measured routing
+(``auto``), so both GEMM paths are pinned against fp32 torch on purpose.
+ERNIE (key-bias padding mask) and ViT (packed-QKV attention, ``pack_dim=2``)
+also run in fp16, the dtype of the reference's O2 recipes
+(``ViT_base_patch16_224_pt_in1k_2n16c_dp_fp16o2.yaml``).
 """
 import os
 
@@ -16,6 +23,15 @@ pytestmark = pytest.mark.gpu
 
 CFG = os.path.join(os.path.dirname(__file__), "..", "fleetx_amd", "configs", "nlp", "gpt",
                    "pretrain_gpt_345M_single_card.yaml")
+
+
+@pytest.fixture(autouse=True, params=["hip", "auto"])
+def gemm_mode(request):
+    from fleetx_amd.ops import gemm as G
+    old = G._MODE
+    G.set_mode(request.param)
+    yield request.param
+    G.set_mode(old)
 
 
 def _rel(a, b):
@@ -171,7 +187,8 @@ def _check_grads(model, P, tol=5e-2):
     assert not bad, bad
 
 
-def test_ernie_bf16_hip_vs_fp32_torch():
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_ernie_hip_vs_fp32_torch(dtype):
     from fleetx_amd.models.language_model.ernie.model import ErnieModel
     from fleetx_amd.parallel import topology as topo
     topo.reset_hcg()
@@ -179,7 +196,7 @@ def test_ernie_bf16_hip_vs_fp32_torch():
     heads, L, V, S, B = 8, 2, 2048, 192, 4
     model = ErnieModel(vocab_size=V, hidden_size=512, num_hidden_layers=L, num_attention_heads=heads,
                        intermediate_size=2048, hidden_dropout_prob=0.0,
-                       attention_probs_dropout_prob=0.0).cuda().to(torch.bfloat16)
+                       attention_probs_dropout_prob=0.0).cuda().to(dtype)
     _perturb(model)
     ids = torch.randint(1, V, (B, S), device="cuda")
     ids[1, 150:] = 0                       # padded tail -> key-bias mask
@@ -196,19 +213,20 @@ def test_ernie_bf16_hip_vs_fp32_torch():
     _check_grads(model, P)
 
 
-def test_vit_bf16_hip_vs_fp32_torch():
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_vit_hip_vs_fp32_torch(dtype):
     from fleetx_amd.models.vision_model.vit import ViT
     torch.manual_seed(2)
     heads, L, patch = 4, 2, 16
     model = ViT(img_size=128, patch_size=patch, class_num=100, embed_dim=256, depth=L,
-                num_heads=heads, qkv_bias=True, epsilon=1e-6).cuda().to(torch.bfloat16)
+                num_heads=heads, qkv_bias=True, epsilon=1e-6).cuda().to(dtype)
     _perturb(model)
     img = torch.randn(8, 3, 128, 128, device="cuda")
     labels = torch.randint(0, 100, (8,), device="cuda")
-    logits = model(img.to(torch.bfloat16))
+    logits = model(img.to(dtype))
     F.cross_entropy(logits.float(), labels).backward()
     P = {n: p.detach().float().clone().requires_grad_(True) for n, p in model.named_parameters()}
-    ref = _vit_reference(P, img.to(torch.bfloat16).float(), heads, L, patch)
+    ref = _vit_reference(P, img.to(dtype).float(), heads, L, patch)
     F.cross_entropy(ref, labels).backward()
     assert _rel(logits, ref) < 3e-2, _rel(logits, ref)
     _check_grads(model, P)

@@ -5,6 +5,12 @@ PP2 1F1B / interleaved, ZeRO-1/2/3, DP -- must reproduce the single-rank bf16
 loss curve: the first step's loss (same weights, no update yet) to bf16
 rounding, later steps within bf16 accumulation-order noise.
 
+Losses alone cannot see a gradient-scale bug (AdamW is invariant to a
+constant gradient scale), so every step also compares the pre-clip global
+gradient norm (a DP/ZeRO "sum instead of mean" doubles it) and, after the
+last step, the global norm of the fp32 master weights against the single-rank
+run.
+
 This is the device-side twin of ``tests/test_distributed_cpu.py``; RCCL itself
 is exercised by the driver's 8-GPU runs."""
 import os
@@ -54,7 +60,7 @@ def _train_gpu(rank, world, layout, steps=3, extra=()):
     drank = hcg.dp_rank * hcg.sharding_degree + hcg.sharding_rank
     g = torch.Generator().manual_seed(7)
     toks = torch.randint(0, VOCAB, (steps, GBS, SEQ + 1), generator=g)
-    losses = []
+    losses, gnorms = [], []
     for s in range(steps):
         t = toks[s, drank * local:(drank + 1) * local].cuda()
         batch = [t[:, :-1].contiguous(),
@@ -62,19 +68,50 @@ def _train_gpu(rank, world, layout, steps=3, extra=()):
                  t[:, 1:].contiguous(), torch.ones(local, SEQ, device="cuda")]
         loss = eng._fit_impl(batch)
         losses.append(eng._reduce_log_loss(loss, 1))
+        gnorms.append(float(eng.optimizer.last_grad_norm))
     torch.cuda.synchronize()
     from fleetx_amd.ops import _lib
-    return {"losses": losses, "drank": drank, "native": _lib.kernels() is not None}
+    return {"losses": losses, "gnorms": gnorms, "pnorm": _master_norm(eng), "drank": drank,
+            "native": _lib.kernels() is not None}
+
+
+def _master_norm(eng):
+    """Global L2 norm of the fp32 master weights, reduced like the gradient
+    norm (mp-sharded ranges summed over mp, owned shards over the ZeRO group,
+    stages over pp; replicated ranges once)."""
+    import torch.distributed as dist
+    opt = eng.optimizer
+    opt.sync_state()
+    dist_sq = torch.zeros((), dtype=torch.float64, device="cuda")
+    rep_sq = torch.zeros((), dtype=torch.float64, device="cuda")
+    for (s, e, c), m in zip(opt.ranges, opt.master):
+        sq = m.double().pow(2).sum()
+        if c.distributed:
+            dist_sq += sq
+        else:
+            rep_sq += sq
+    buf = opt.buffer
+    if buf.shard_stage >= 1 and buf.shard_group is not None:
+        pair = torch.stack([dist_sq, rep_sq])
+        dist.all_reduce(pair, group=buf.shard_group.group)
+        dist_sq, rep_sq = pair[0], pair[1]
+    if opt.mp_group is not None:
+        dist.all_reduce(dist_sq, group=opt.mp_group.group)
+    total = dist_sq + rep_sq
+    if opt.pp_group is not None:
+        dist.all_reduce(total, group=opt.pp_group.group)
+    return float(total.sqrt())
 
 
 @pytest.fixture(scope="module")
 def ref_gpu():
     r = dist_utils.run(_train_gpu, 1, (1, 1, 1, 1, 0, GBS, False, 1), timeout=300)
     assert r[0]["native"]
-    return r[0]["losses"]
+    return r[0]
 
 
-def _check(results, ref):
+def _check(results, ref_run):
+    ref = ref_run["losses"]
     by = {}
     for r in results:
         by.setdefault(r["drank"], r["losses"])
@@ -83,6 +120,16 @@ def _check(results, ref):
     assert abs(got[0] - ref[0]) < 2e-3 * abs(ref[0]), (got, ref)
     for a, b in zip(got[1:], ref[1:]):
         assert abs(a - b) < 1.5e-2 * abs(b), (got, ref)
+    # gradient scale: the global pre-clip norm is the same on every rank and
+    # matches the single-rank run (a missing 1/dp would double it)
+    for r in results:
+        g, gr = r["gnorms"], ref_run["gnorms"]
+        assert abs(g[0] - gr[0]) < 2e-2 * gr[0], (g, gr)
+        for a, b in zip(g[1:], gr[1:]):
+            assert abs(a - b) < 5e-2 * b, (g, gr)
+        # fp32 master weights after the last update
+        assert abs(r["pnorm"] - ref_run["pnorm"]) < 1e-3 * ref_run["pnorm"], \
+            (r["pnorm"], ref_run["pnorm"])
 
 
 LAYOUTS = {

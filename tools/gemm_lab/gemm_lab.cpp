@@ -51,6 +51,7 @@ int main(int argc, char** argv) {
         {"fwd", 0, 0, 0, M, N, K, x, K, w, K, c16, N},
         {"fwd_gelu", 0, 0, 1, M, N, K, x, K, w, K, c16, N},
         {"dgrad", 0, 1, 0, M, K, N, dy, N, w, K, c16, K},
+        {"dgrad_dgelu", 0, 1, 2, M, K, N, dy, N, w, K, c16, K},
         {"wgrad", 1, 1, 3, N, K, M, dy, N, x, K, c32, K},
     };
     printf("{\"gemm\": \"%s\"", s.name);
