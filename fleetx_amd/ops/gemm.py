@@ -49,9 +49,10 @@ def set_mode(mode):
 #  * wgrad: the fp32-accumulating weight gradient in its native token-major
 #    layout -- 1.23-1.43 PF against 1.01-1.18 PF for hipBLASLt's TN path plus
 #    the two transposes it needs (profiles/r3_gemm/);
-#  * dgrad: the data gradient with the weight read in place (hardware
-#    transposed LDS reads) -- 1.41-1.54 PF against 1.41-1.48 PF for the TN
-#    path with its weight transpose;
+#  * dgrad (opt-in): the data gradient with the weight read in place
+#    (hardware transposed LDS reads) -- 1.37-1.54 PF against 1.41-1.48 PF for
+#    the TN path with its weight transpose in isolation, but 4 ms/step slower
+#    in the 6.7B step on the same box (profiles/r3_step/routing_ab.txt);
 #  * dgrad_act / fwd_act (opt-in): the GEMMs with a fused GeLU' / bias+GeLU
 #    epilogue.  Measured in the 6.7B step they lose: the GeLU math runs with
 #    the matrix pipe idle at one workgroup per CU (0.97 ms vs 0.77 ms for the
@@ -61,7 +62,7 @@ def set_mode(mode):
 # forward GEMMs stay on hipBLASLt, whose TN kernels tie or lead there.
 # Only shapes whose output fills the chip (>= 192 tiles of 256 x 256 on the
 # 256 CUs) go to the kernel; FLEETX_GEMM_AUTO="kind,kind" replaces the set.
-_DEFAULT_AUTO = "wgrad,dgrad"
+_DEFAULT_AUTO = "wgrad"
 AUTO_KINDS = set(k for k in os.environ.get("FLEETX_GEMM_AUTO", _DEFAULT_AUTO).split(",") if k)
 MIN_TILES = int(os.environ.get("FLEETX_GEMM_MIN_TILES", "192"))
 

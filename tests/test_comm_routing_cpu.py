@@ -40,9 +40,8 @@ def test_gemm_routing_table():
         assert G.out_tiles("wgrad", t(8192, 12288), x) == 48 * 16
         assert G.use("wgrad", t(8192, 12288), x) and G.use("wgrad", t(8192, 4096), x)
         assert not G.use("fwd_act", x, t(16384, 4096))          # opt-in (FLEETX_GEMM_AUTO)
-        assert G.use("dgrad", t(8192, 12288), w_qkv)
-        # plain forward GEMMs stay on hipBLASLt
-        assert not G.use("fwd", x, w_qkv)
+        # forward and data-gradient GEMMs stay on hipBLASLt by default
+        assert not G.use("fwd", x, w_qkv) and not G.use("dgrad", t(8192, 12288), w_qkv)
         # 1.3B out-proj wgrad (64 tiles) and 345M shapes under-fill the chip
         assert not G.use("wgrad", t(8192, 2048), t(8192, 2048))
         assert not G.use("wgrad", t(8192, 1024), t(8192, 1024))
