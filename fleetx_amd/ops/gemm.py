@@ -60,27 +60,30 @@ def set_mode(mode):
 #    pass they retire), and a forward GEMM that holds whole CUs starves the
 #    forward-overlapped AdamW (profiles/r3_step/);
 # forward GEMMs stay on hipBLASLt, whose TN kernels tie or lead there.
-# Only shapes whose output fills the chip (>= 192 tiles of 256 x 256 on the
-# 256 CUs) go to the kernel; FLEETX_GEMM_AUTO="kind,kind" replaces the set.
+# Only shapes whose output fills the chip go to the kernel: >= 192 tiles of
+# 128 x 128 (the kernel itself runs 256 x 256 tiles when there are >= 192 of
+# those, else 128 x 128 tiles at two workgroups per CU, which is what the
+# hidden 1024-2048 models and ViT-g use); FLEETX_GEMM_AUTO="kind,kind"
+# replaces the set.
 _DEFAULT_AUTO = "wgrad"
 AUTO_KINDS = set(k for k in os.environ.get("FLEETX_GEMM_AUTO", _DEFAULT_AUTO).split(",") if k)
 MIN_TILES = int(os.environ.get("FLEETX_GEMM_MIN_TILES", "192"))
 
 
-def _tiles(r, c):
-    return ((r + 255) // 256) * ((c + 255) // 256)
+def _tiles(r, c, t=128):
+    return ((r + t - 1) // t) * ((c + t - 1) // t)
 
 
-def out_tiles(kind, a, b):
-    """256 x 256 output tiles of GEMM ``kind`` on operands (a, b) as passed to
+def out_tiles(kind, a, b, t=128):
+    """t x t output tiles of GEMM ``kind`` on operands (a, b) as passed to
     :func:`use`: fwd (x, w) -> [M, N]; dgrad (dy, w) -> [M, K]; wgrad (dy, x)
     -> [N, K]."""
     M = a.numel() // a.shape[-1]
     if kind.startswith("fwd"):
-        return _tiles(M, b.shape[0])
+        return _tiles(M, b.shape[0], t)
     if kind.startswith("dgrad"):
-        return _tiles(M, b.shape[1])
-    return _tiles(a.shape[-1], b.shape[-1])
+        return _tiles(M, b.shape[1], t)
+    return _tiles(a.shape[-1], b.shape[-1], t)
 
 
 def use(kind, a, b=None):

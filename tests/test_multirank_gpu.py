@@ -78,13 +78,16 @@ def _train_gpu(rank, world, layout, steps=3, extra=()):
 def _master_norm(eng):
     """Global L2 norm of the fp32 master weights, reduced like the gradient
     norm (mp-sharded ranges summed over mp, owned shards over the ZeRO group,
-    stages over pp; replicated ranges once)."""
+    stages over pp; replicated ranges once, the pipeline's duplicate of the
+    tied embedding not at all)."""
     import torch.distributed as dist
     opt = eng.optimizer
     opt.sync_state()
     dist_sq = torch.zeros((), dtype=torch.float64, device="cuda")
     rep_sq = torch.zeros((), dtype=torch.float64, device="cuda")
     for (s, e, c), m in zip(opt.ranges, opt.master):
+        if c.norm_excluded:  # the last stage's copy of the tied embedding (counted once)
+            continue
         sq = m.double().pow(2).sum()
         if c.distributed:
             dist_sq += sq

@@ -31,7 +31,7 @@ int main(int argc, char** argv) {
   const int iters = argc > 2 ? atoi(argv[2]) : 20;
   const char* stamp_case = argc > 3 ? argv[3] : nullptr;  // e.g. "out:fwd": dump stamps
   fx_gemm_set_variant(variant);
-  const int T = 8192, H = 4096;
+  const int T = 8192, H = getenv("LAB_H") ? atoi(getenv("LAB_H")) : 4096;
   struct Sh { const char* name; int K, N; } shapes[] = {
       {"qkv", H, 3 * H}, {"out", H, H}, {"fc1", H, 4 * H}, {"fc2", 4 * H, H}};
   size_t maxe = (size_t)T * 4 * H;

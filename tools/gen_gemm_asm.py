@@ -41,8 +41,27 @@ import sys
 KC, MC = 0, 1
 # schedule knobs (per generated stream): dma_off = this wave's DMA slot shift
 CFG = {"dma_off": 0, "dma_start": 0, "stagger": 1}
-FRAG_BASE = {("A", 0): 128, ("A", 1): 160, ("B", 0): 192, ("B", 1): 224}
-BUF = 65536
+# Geometry of the stream being generated (set_geometry):
+#   T256: 256 x 256 workgroup tile, 4 waves of 128 x 128 (8 x 8 fragments),
+#         fragments in v[128:255], two 64 KiB LDS buffers, 1 workgroup per CU;
+#   T128: 128 x 128 tile, 4 waves of 64 x 64 (4 x 4 fragments), fragments in
+#         v[64:127], two 32 KiB buffers, 2 workgroups per CU (their waves
+#         cover each other's LDS-DMA issue).
+GEO = {}
+
+
+def set_geometry(tag):
+    nf = 8 if tag == "T256" else 4
+    fb = 128 if nf == 8 else 64
+    n = 4 * nf  # registers per (operand, k-step) fragment set
+    GEO.clear()
+    GEO.update(tag=tag, nf=nf, buf=2 * (32 * nf) * 128,
+               frag_base={("A", 0): fb, ("A", 1): fb + n, ("B", 0): fb + 2 * n,
+                          ("B", 1): fb + 3 * n})
+
+
+def FRAG(op, s):
+    return GEO["frag_base"][(op, s)]
 
 
 class Stream:
@@ -84,7 +103,7 @@ def vreg(base, n):
 def read_ops(lay, op, s, i, which):
     """LDS reads of fragment i (k-step s) of operand op ('A'/'B') from the
     buffer addressed by base set `which` ('cur' / 'nxt')."""
-    dst = FRAG_BASE[(op, s)] + 4 * i
+    dst = FRAG(op, s) + 4 * i
     key = (op, s, i)
     if lay == KC:
         base = "%%[r%s_%s]" % (op, which)   # KC bases: cur = k-step 1, nxt = k-step 0
@@ -97,16 +116,17 @@ def read_ops(lay, op, s, i, which):
 
 
 def dma_ops(op, nop=False):
-    """8 LDS-DMA loads of operand op for the next-but-one K-tile (M0 = this
-    wave's 8 KiB slice of the operand's region in the buffer being refilled).
+    """nf LDS-DMA loads of operand op for the next-but-one K-tile (M0 = this
+    wave's nf KiB slice of the operand's region in the buffer being refilled).
     Returns (m0_setup, [[load, m0 advance], ...]).  An SALU write of M0 needs
     one wait state before an LDS-DMA reads it: in the loop the advance is
     followed by MFMAs; `nop` pads it for back-to-back issue."""
     pad = ["s_nop 0"] if nop else []
     groups = []
-    for u in range(8):
+    nu = GEO["nf"]
+    for u in range(nu):
         g = ["buffer_load_dwordx4 %%[vo%s%d], %%[rs%s], %%[so%s] offen lds" % (op, u, op, op)]
-        if u < 7:
+        if u < nu - 1:
             g += ["s_add_u32 m0, m0, 1024"] + pad
         groups.append(g)
     return ["s_mov_b32 m0, %%[m%s]" % op, "s_nop 0"], groups
@@ -114,19 +134,19 @@ def dma_ops(op, nop=False):
 
 def mfma(dt, st, s, i, j):
     st.need({("A", s, i), ("B", s, j)})
-    k = 8 * i + j
+    k = GEO["nf"] * i + j
     mn = "v_mfma_f32_16x16x32_bf16" if dt == "bf16" else "v_mfma_f32_16x16x32_f16"
-    st.emit("%s %%%d, %s, %s, %%%d" % (mn, k, vreg(FRAG_BASE[("B", s)] + 4 * j, 4),
-                                       vreg(FRAG_BASE[("A", s)] + 4 * i, 4), k))
+    st.emit("%s %%%d, %s, %s, %%%d" % (mn, k, vreg(FRAG("B", s) + 4 * j, 4),
+                                       vreg(FRAG("A", s) + 4 * i, 4), k))
 
 
 def segment(dt, st, s, rows, extras, read_gap, dma_gap, close=None):
-    """MFMAs of k-step s for fragment rows `rows` (x 8 columns) with `extras`
+    """MFMAs of k-step s for fragment rows `rows` (x nf columns) with `extras`
     (list of ('read', [(key, text)...]) / ('dma', (setup, groups))) interleaved:
     reads one per `read_gap` MFMAs from the start, DMA loads one per `dma_gap`
     MFMAs.  `close` = wait line ('lgkm0' = drain the scoreboard) emitted before
     the last MFMA, followed by s_barrier after it."""
-    mf = [(s, i, j) for i in rows for j in range(8)]
+    mf = [(s, i, j) for i in rows for j in range(GEO["nf"])]
     reads = [x for kind, xs in extras if kind == "read" for x in xs]
     setup, groups = [], []
     for kind, xs in extras:
@@ -164,6 +184,7 @@ def segment(dt, st, s, rows, extras, read_gap, dma_gap, close=None):
 def generate(la, lb, dt, read_gap=1, dma_gap=3):
     lay = {"A": la, "B": lb}
     out = []
+    nf, X = GEO["nf"], "0x%x" % GEO["buf"]
     out.append("s_mov_b32 %[keep], m0")
     # prologue: tiles 0 and 1 (B then A each), tile 0's k0 fragments
     for t in range(2):
@@ -173,21 +194,21 @@ def generate(la, lb, dt, read_gap=1, dma_gap=3):
             for g in groups:
                 out += g
             out.append("s_add_u32 %%[so%s], %%[so%s], %%[ks%s]" % (op, op, op))
-            out.append("s_xor_b32 %%[m%s], %%[m%s], 0x10000" % (op, op))
-    out.append("s_waitcnt vmcnt(16)")
+            out.append("s_xor_b32 %%[m%s], %%[m%s], %s" % (op, op, X))
+    out.append("s_waitcnt vmcnt(%d)" % (2 * nf))
     out.append("s_barrier")
     pro = Stream()
     for op in "BA":
-        for i in range(8):
+        for i in range(nf):
             for key, text in read_ops(lay[op], op, 0, i, "nxt"):
                 pro.read(key, text)
     out += pro.lines
     for op in "AB":
         if lay[op] == KC:
-            out.append("v_xor_b32 %%[r%s_nxt], 0x10000, %%[r%s_nxt]" % (op, op))
+            out.append("v_xor_b32 %%[r%s_nxt], %s, %%[r%s_nxt]" % (op, X, op))
         else:
-            out.append("v_xor_b32 %%[r%s_nxtlo], 0x10000, %%[r%s_nxtlo]" % (op, op))
-            out.append("v_xor_b32 %%[r%s_nxthi], 0x10000, %%[r%s_nxthi]" % (op, op))
+            out.append("v_xor_b32 %%[r%s_nxtlo], %s, %%[r%s_nxtlo]" % (op, X, op))
+            out.append("v_xor_b32 %%[r%s_nxthi], %s, %%[r%s_nxthi]" % (op, X, op))
     # The fragments of k-step 0 of the coming tile are the last reads issued
     # before every body (prologue or previous body); each body starts from
     # that scoreboard.
@@ -235,31 +256,33 @@ def body_with(st, la, lb, dt, kind, read_gap, dma_gap):
         return ("read", [r for i in idxs for r in read_ops(lay[op], op, s, i, which)])
 
     full, last = kind == "full", kind == "last"
-    segment(dt, st, 0, range(0, 4), [reads("B", 1, "cur", range(8))], read_gap, dma_gap,
+    nf, X = GEO["nf"], "0x%x" % GEO["buf"]
+    h, q = nf // 2, nf // 4
+    segment(dt, st, 0, range(0, h), [reads("B", 1, "cur", range(nf))], read_gap, dma_gap,
             close=None if last else "lgkm0")
-    ex = [reads("A", 1, "cur", range(8))]
+    ex = [reads("A", 1, "cur", range(nf))]
     if full:
         ex.append(("dma", dma_ops("B")))
-    segment(dt, st, 0, range(4, 8), ex, read_gap, dma_gap, close=None if last else "lgkm0")
+    segment(dt, st, 0, range(h, nf), ex, read_gap, dma_gap, close=None if last else "lgkm0")
     ex = [("dma", dma_ops("A"))] if full else []
-    close = None if last else "s_waitcnt vmcnt(%d)" % (24 if full else 8)
-    segment(dt, st, 1, range(0, 4), ex, read_gap, dma_gap, close=close)
+    close = None if last else "s_waitcnt vmcnt(%d)" % (3 * nf if full else nf)
+    segment(dt, st, 1, range(0, h), ex, read_gap, dma_gap, close=close)
     if last:
-        segment(dt, st, 1, range(4, 8), [], read_gap, dma_gap)
+        segment(dt, st, 1, range(h, nf), [], read_gap, dma_gap)
         st.emit("s_nop 15")
         st.emit("s_nop 15")
         return st.lines, st.pending
-    segment(dt, st, 1, range(4, 6), [reads("B", 0, "nxt", range(8))], 1, dma_gap,
-            close="s_waitcnt vmcnt(%d)" % (16 if full else 0))
-    segment(dt, st, 1, range(6, 8), [reads("A", 0, "nxt", range(8))], 1, dma_gap)
+    segment(dt, st, 1, range(h, h + q), [reads("B", 0, "nxt", range(nf))], 1, dma_gap,
+            close="s_waitcnt vmcnt(%d)" % (2 * nf if full else 0))
+    segment(dt, st, 1, range(h + q, nf), [reads("A", 0, "nxt", range(nf))], 1, dma_gap)
     for op in "AB":
         if lay[op] == KC:
-            st.emit("v_xor_b32 %%[r%s_cur], 0x10000, %%[r%s_cur]" % (op, op))
-            st.emit("v_xor_b32 %%[r%s_nxt], 0x10000, %%[r%s_nxt]" % (op, op))
+            st.emit("v_xor_b32 %%[r%s_cur], %s, %%[r%s_cur]" % (op, X, op))
+            st.emit("v_xor_b32 %%[r%s_nxt], %s, %%[r%s_nxt]" % (op, X, op))
         else:
             for w in ("curlo", "curhi", "nxtlo", "nxthi"):
-                st.emit("v_xor_b32 %%[r%s_%s], 0x10000, %%[r%s_%s]" % (op, w, op, w))
-        st.emit("s_xor_b32 %%[m%s], %%[m%s], 0x10000" % (op, op))
+                st.emit("v_xor_b32 %%[r%s_%s], %s, %%[r%s_%s]" % (op, w, X, op, w))
+        st.emit("s_xor_b32 %%[m%s], %%[m%s], %s" % (op, op, X))
         if full:
             st.emit("s_add_u32 %%[so%s], %%[so%s], %%[ks%s]" % (op, op, op))
     return st.lines, st.pending
@@ -294,19 +317,25 @@ def main():
     path = os.environ.get("FX_GEN_OUT") or os.path.join(here, "..", "csrc", "kernels",
                                                         "gemm_asm.inc")
     read_gap = int(os.environ.get("FX_GEN_READ_GAP", "1"))
-    dma_gap = int(os.environ.get("FX_GEN_DMA_GAP", "4"))
+    # T256: one DMA per 4 MFMAs, wave-staggered slots; T128 (8-MFMA segments):
+    # one per 2 MFMAs, no stagger
+    knobs = {"T256": (int(os.environ.get("FX_GEN_DMA_GAP", "4")),
+                      int(os.environ.get("FX_GEN_STAGGER", "1"))),
+             "T128": (int(os.environ.get("FX_GEN_DMA_GAP_T128", "2")), 0)}
     CFG["dma_start"] = int(os.environ.get("FX_GEN_DMA_START", "0"))
-    CFG["stagger"] = int(os.environ.get("FX_GEN_STAGGER", "1"))
     parts = ["// GENERATED by tools/gen_gemm_asm.py -- do not edit.\n"
-             "// K-loop of gemm5_kernel (csrc/kernels/gemm5.hip); read_gap=%d dma_gap=%d stagger=%d\n"
-             % (read_gap, dma_gap, CFG["stagger"])]
+             "// K-loops of gemm5_kernel (csrc/kernels/gemm5.hip); read_gap=%d, "
+             "(dma_gap, stagger) T256=%s T128=%s\n" % (read_gap, knobs["T256"], knobs["T128"])]
     names = {KC: "KC", MC: "MC"}
-    for la, lb in ((KC, KC), (KC, MC), (MC, MC)):
-        for dt in ("bf16", "f16"):
-            lines = ablate(generate(la, lb, dt, read_gap, dma_gap))
-            parts.append("#define FX_GEMM5_LOOP_%s_%s_%s \\\n%s\n" % (
-                names[la], names[lb], dt.upper(),
-                " \\\n".join('  "%s\\n"' % l for l in lines)))
+    for tag in ("T256", "T128"):
+        set_geometry(tag)
+        dma_gap, CFG["stagger"] = knobs[tag]
+        for la, lb in ((KC, KC), (KC, MC), (MC, MC)):
+            for dt in ("bf16", "f16"):
+                lines = ablate(generate(la, lb, dt, read_gap, dma_gap))
+                parts.append("#define FX_G5_%s_%s_%s_%s \\\n%s\n" % (
+                    tag, names[la], names[lb], dt.upper(),
+                    " \\\n".join('  "%s\\n"' % l for l in lines)))
     with open(path, "w") as f:
         f.write("\n".join(parts))
     print("wrote", os.path.normpath(path), file=sys.stderr)
