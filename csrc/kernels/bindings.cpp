@@ -35,7 +35,7 @@ void fx_ce_bwd(int, const void*, void*, const int64_t*, const float*, const floa
                int, hipStream_t);
 int fx_sumsq_blocks(long n);
 void fx_sumsq_f32(const float*, long, float*, int, hipStream_t);
-void fx_adamw_tune(int, int);
+void fx_adamw_tune(int, int, int);
 void fx_adamw_flat(int, float*, const float*, float*, float*, void*, long, float, float, float,
                    float, float, float, const float*, const int*, const int*, hipStream_t);
 void fx_cast_f32(int, const float*, void*, long, hipStream_t);
@@ -157,7 +157,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("sumsq_f32", [](ptr x, long n, ptr partial, int blocks, ptr st) {
     fx_sumsq_f32(F(x), n, F(partial), blocks, S(st));
   });
-  m.def("adamw_tune", &fx_adamw_tune);
+  m.def("adamw_tune", &fx_adamw_tune, py::arg("grid"), py::arg("nt"), py::arg("wide") = 0);
   m.def("adamw_flat", [](int dt, ptr p, ptr g, ptr mm, ptr vv, ptr p16, long n, float lr,
                          float b1, float b2, float eps, float wd, float l2, ptr gscale, ptr skip,
                          ptr step, ptr st) {

@@ -151,8 +151,13 @@ __device__ __forceinline__ void st_stream(V x, V* a, bool nt) {
   if (nt) __builtin_nontemporal_store(x, a); else *a = x;
 }
 
-template <typename T, bool NT>
-__global__ __launch_bounds__(256) void adamw_flat_kernel(
+// BS threads per block, U float4 groups per thread per pass (4U x 16-byte
+// loads in flight per lane).  The default (256, 2) fills the chip; the
+// forward-overlapped update runs (1024, 4) on a capped grid instead: few CUs,
+// each with 256 KiB of loads in flight, so the GEMMs beside it keep the rest
+// of the chip (optims/optimizer.py, _update_overlapped).
+template <typename T, bool NT, int BS, int U>
+__global__ __launch_bounds__(BS) void adamw_flat_kernel(
     float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
     float* __restrict__ v, uint16_t* __restrict__ p16, long n, float lr, float beta1,
     float beta2, float eps, float wd, float l2, const float* __restrict__ gscale,
@@ -167,25 +172,23 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(
   const float inv_sqrt_bc2 = rsqrtf(bc2);
   const float decay = 1.f - lr * wd;
   const long n4 = n / 4;
-  const long stride = (long)gridDim.x * 512;
-  for (long i0 = blockIdx.x * 512L + threadIdx.x; i0 < n4; i0 += stride) {
-    const long i1 = i0 + 256;
-    const bool two = i1 < n4;
-    floatx4 pp[2], gg[2], mm[2], vv[2];
-    pp[0] = ld_stream(reinterpret_cast<const floatx4*>(p) + i0, NT);
-    gg[0] = ld_stream(reinterpret_cast<const floatx4*>(g) + i0, NT);
-    mm[0] = ld_stream(reinterpret_cast<const floatx4*>(m) + i0, NT);
-    vv[0] = ld_stream(reinterpret_cast<const floatx4*>(v) + i0, NT);
-    if (two) {
-      pp[1] = ld_stream(reinterpret_cast<const floatx4*>(p) + i1, NT);
-      gg[1] = ld_stream(reinterpret_cast<const floatx4*>(g) + i1, NT);
-      mm[1] = ld_stream(reinterpret_cast<const floatx4*>(m) + i1, NT);
-      vv[1] = ld_stream(reinterpret_cast<const floatx4*>(v) + i1, NT);
+  const long stride = (long)gridDim.x * (BS * U);
+  for (long i0 = blockIdx.x * (long)(BS * U) + threadIdx.x; i0 < n4; i0 += stride) {
+    floatx4 pp[U], gg[U], mm[U], vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long i = i0 + (long)u * BS;
+      if (i < n4) {
+        pp[u] = ld_stream(reinterpret_cast<const floatx4*>(p) + i, NT);
+        gg[u] = ld_stream(reinterpret_cast<const floatx4*>(g) + i, NT);
+        mm[u] = ld_stream(reinterpret_cast<const floatx4*>(m) + i, NT);
+        vv[u] = ld_stream(reinterpret_cast<const floatx4*>(v) + i, NT);
+      }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (u == 1 && !two) break;
-      const long i = u ? i1 : i0;
+    for (int u = 0; u < U; ++u) {
+      const long i = i0 + (long)u * BS;
+      if (i >= n4) break;
       floatx4 pa = pp[u], ma = mm[u], va = vv[u];
       const floatx4 ga = gg[u];
 #pragma unroll
@@ -209,7 +212,7 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(
       }
     }
   }
-  for (long i = n4 * 4 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+  for (long i = n4 * 4 + blockIdx.x * (long)BS + threadIdx.x; i < n; i += (long)gridDim.x * BS) {
     const float gr = g[i] * gs + l2 * p[i];
     m[i] = beta1 * m[i] + (1.f - beta1) * gr;
     v[i] = beta2 * v[i] + (1.f - beta2) * gr * gr;
@@ -359,32 +362,46 @@ extern "C" void fx_sumsq_f32(const float* x, long n, float* partial, int blocks,
   sumsq_f32_kernel<<<blocks, 256, 0, st>>>(x, n, partial);
 }
 
-static int g_adamw_grid = 0, g_adamw_nt = 1;  // tuning knobs (tools/bench_optim.py)
+static int g_adamw_grid = 0, g_adamw_nt = 1, g_adamw_wide = 0;  // tuning knobs
 static const float* g_adamw_lr = nullptr;     // graph mode: device learning rate
 extern "C" void fx_set_adamw_lr_ptr(const void* p) { g_adamw_lr = (const float*)p; }
-extern "C" void fx_adamw_tune(int grid, int nt) {
+// grid: workgroup cap (0 = fill the chip); nt: non-temporal accesses;
+// wide: 1 = 1024-thread blocks with 4 float4 groups per thread (the capped,
+// forward-overlapped update), 0 = 256 x 2
+extern "C" void fx_adamw_tune(int grid, int nt, int wide) {
   g_adamw_grid = grid;
   g_adamw_nt = nt;
+  g_adamw_wide = wide;
+}
+
+template <typename T, bool NT, int BS, int U>
+static void adamw_launch(float* p, const float* g, float* m, float* v, void* p16, long n,
+                         float lr, float beta1, float beta2, float eps, float wd, float l2,
+                         const float* gscale, const int* skip, const int* step, hipStream_t st) {
+  // at most 8 resident 256-thread blocks per CU (2 of 1024)
+  const long per = (long)BS * U * 4;
+  long blocks = (n + per - 1) / per;
+  const long cap = 256L * (8 * 256 / BS) * 4;
+  int grid = (int)(blocks < 1 ? 1 : (blocks > cap ? cap : blocks));
+  if (g_adamw_grid > 0 && g_adamw_grid < grid) grid = g_adamw_grid;
+  adamw_flat_kernel<T, NT, BS, U><<<grid, BS, 0, st>>>(p, g, m, v, (uint16_t*)p16, n, lr, beta1,
+                                                      beta2, eps, wd, l2, gscale, skip, step,
+                                                      g_adamw_lr);
 }
 
 extern "C" void fx_adamw_flat(int dtype, float* p, const float* g, float* m, float* v, void* p16,
                               long n, float lr, float beta1, float beta2, float eps, float wd,
                               float l2, const float* gscale, const int* skip, const int* step,
                               hipStream_t st) {
-  // two float4 groups per thread per pass; at most 8 resident 256-thread blocks per CU
-  long blocks = (n / 4 + 511) / 512;
-  const long cap = 256L * 8 * 4;
-  int grid = (int)(blocks < 1 ? 1 : (blocks > cap ? cap : blocks));
-  if (g_adamw_grid > 0 && g_adamw_grid < grid) grid = g_adamw_grid;
-  if (g_adamw_nt) {
-    FX_DISPATCH_T(dtype, adamw_flat_kernel<T, true><<<grid, 256, 0, st>>>(
-                             p, g, m, v, (uint16_t*)p16, n, lr, beta1, beta2, eps, wd, l2,
-                             gscale, skip, step, g_adamw_lr));
+#define FX_ADAMW_ARGS p, g, m, v, p16, n, lr, beta1, beta2, eps, wd, l2, gscale, skip, step, st
+  if (g_adamw_wide) {
+    FX_DISPATCH_T(dtype, adamw_launch<T, true, 1024, 4>(FX_ADAMW_ARGS));
+  } else if (g_adamw_nt) {
+    FX_DISPATCH_T(dtype, adamw_launch<T, true, 256, 2>(FX_ADAMW_ARGS));
   } else {
-    FX_DISPATCH_T(dtype, adamw_flat_kernel<T, false><<<grid, 256, 0, st>>>(
-                             p, g, m, v, (uint16_t*)p16, n, lr, beta1, beta2, eps, wd, l2,
-                             gscale, skip, step, g_adamw_lr));
+    FX_DISPATCH_T(dtype, adamw_launch<T, false, 256, 2>(FX_ADAMW_ARGS));
   }
+#undef FX_ADAMW_ARGS
 }
 
 extern "C" void fx_cast_f32(int dtype, const float* x, void* y, long n, hipStream_t st) {

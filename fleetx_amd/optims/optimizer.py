@@ -159,6 +159,7 @@ class FlatOptimizer:
     # ------------------------------------------------------------------ overlap
     _overlap_groups = None
     overlap_grid = 128  # Distributed.comm.overlap_optimizer_grid
+    overlap_wide = False  # Distributed.comm.overlap_optimizer_wide: 1024-thread blocks
 
     def enable_forward_overlap(self, model):
         """Run the parameter update of step N on a side stream, unit by unit
@@ -286,8 +287,9 @@ class FusedAdamW(FlatOptimizer):
         # with the forward (6.7B step -1.5..-1.8 % on two boxes,
         # profiles/r2_final/adamw_overlap_grid.txt).  0 = uncapped.
         grid = int(os.environ.get("FLEETX_ADAMW_OVERLAP_GRID", str(self.overlap_grid)))
+        wide = int(os.environ.get("FLEETX_ADAMW_OVERLAP_WIDE", str(int(self.overlap_wide))))
         if grid:
-            k.adamw_tune(grid, 1)
+            k.adamw_tune(grid, 1, wide)
         with torch.cuda.stream(os_):
             st = _lib.stream()
             for u, pieces in self._overlap_groups:
@@ -304,7 +306,7 @@ class FusedAdamW(FlatOptimizer):
                 ev.record(os_)
                 self._unit_events[u] = ev
         if grid:
-            k.adamw_tune(0, 1)
+            k.adamw_tune(0, 1, 0)
 
     def _update_offloaded(self, lr):
         """Stream host-resident master/m/v through the GPU in chunks: the H2D

@@ -18,6 +18,8 @@ def main():
     ap.add_argument("--n", type=float, default=1e9)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--sweep", action="store_true", help="grid / non-temporal variants")
+    ap.add_argument("--capped", action="store_true",
+                    help="capped grids (32-128 workgroups) in both block shapes")
     a = ap.parse_args()
     from fleetx_amd.ops import _lib
     k = _lib.kernels()
@@ -57,14 +59,24 @@ def main():
                       "TB_s": round(12.0 * n / ms / 1e9, 3)}))
     m.zero_()
     v.zero_()
-    for grid, nt in ((0, 1), (0, 0), (1024, 1), (2048, 1), (4096, 1), (2048, 0)):
-        if a.sweep or (grid, nt) == (0, 1):
-            k.adamw_tune(grid, nt)
-            ms = timeit(run)
-            print(json.dumps({"kernel": "adamw_flat", "grid": grid or "auto", "nontemporal": nt,
-                              "n": n, "ms": round(ms, 3), "TB_s": round(30.0 * n / ms / 1e9, 3),
-                              "ms_per_6.65B_params": round(ms * 6.65e9 / n, 2)}))
-    k.adamw_tune(0, 1)
+    cases = [(0, 1, 0)]
+    if a.sweep:
+        cases += [(0, 0, 0), (1024, 1, 0), (2048, 1, 0), (4096, 1, 0)]
+    if a.capped:
+        # the forward-overlapped update: few workgroups (CUs), deep per-CU
+        # memory-level parallelism -- bandwidth per CU decides how much of the
+        # chip the update takes from the GEMMs beside it
+        cases += [(g, 1, w) for w in (0, 1) for g in (32, 48, 64, 96, 128)]
+    for grid, nt, wide in cases:
+        k.adamw_tune(grid, nt, wide)
+        ms = timeit(run)
+        tb = 30.0 * n / ms / 1e9
+        print(json.dumps({"kernel": "adamw_flat", "grid": grid or "auto", "nontemporal": nt,
+                          "block": 1024 if wide else 256, "float4_per_thread": 4 if wide else 2,
+                          "n": n, "ms": round(ms, 3), "TB_s": round(tb, 3),
+                          "GB_s_per_workgroup": round(1000 * tb / grid, 1) if grid else None,
+                          "ms_per_6.65B_params": round(ms * 6.65e9 / n, 2)}))
+    k.adamw_tune(0, 1, 0)
 
 
 if __name__ == "__main__":
