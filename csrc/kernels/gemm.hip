@@ -1294,8 +1294,15 @@ extern "C" void fx_gemm_set_debug(unsigned long long* p) { g_dbg = p; }
 //   -4: an operand too large for 32-bit per-lane offsets.
 extern "C" int fx_gemm(int dt, int la, int lb, int epi, int M, int N, int K, const void* A,
                        long lda, const void* B, long ldb, void* C, long ldc, const void* bias,
-                       void* aux, long ldaux, int beta, hipStream_t st) {
+                       void* aux, long ldaux, int beta, hipStream_t st, float* sq) {
   if (M <= 0 || N <= 0 || K <= 0 || K % BK) return -1;
+  if (sq != nullptr) {  // norm partials: the hand-scheduled kernel's fp32 epilogue only
+    if (g_variant < 0) {
+      const char* e = getenv("FLEETX_GEMM_PF");
+      g_variant = e ? atoi(e) : 5;
+    }
+    if (epi != EPI_F32 || g_variant != 5 || K < 2 * BK) return -5;
+  }
   if (N % 4 || (la == LAY_MC && M % 8) || (lb == LAY_MC && N % 8)) return -2;
   if (M < 8 || N < 8) return -2;
   const long a_span = la == LAY_KC ? (long)M * lda : (long)BK * lda + M;
@@ -1320,5 +1327,6 @@ extern "C" int fx_gemm(int dt, int la, int lb, int epi, int M, int N, int K, con
   }
   P.gm = g_gm > 0 ? g_gm : 8;
   P.dbg = g_dbg;
+  P.sq = sq;
   return dt == 0 ? dispatch<bf16>(la, lb, epi, P, st) : dispatch<f16>(la, lb, epi, P, st);
 }

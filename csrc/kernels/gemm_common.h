@@ -27,6 +27,10 @@ struct GemmParams {
   int beta;
   int gm;  // tiles per M-group of the block order (L2 reuse)
   unsigned long long* dbg;  // tools/gemm_lab timeline stamps (FX_GEMM_STAMP builds only)
+  // EPI_F32 (gemm5 only): per-wave sums of squares of the stored values,
+  // sq[4 * blockIdx.x + wave] -- the gradient-norm partials of a weight
+  // gradient, taken from the accumulators instead of re-reading main_grad
+  float* sq;
 };
 
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {

@@ -248,6 +248,11 @@ class EagerEngine(BasicEngine):
             if comm.get("early_grad_norm", False) and not self._pipeline and not self._cuda_graph \
                     and hasattr(self.buffer, "enable_early_norm"):
                 self.buffer.enable_early_norm()
+            # otherwise the weight-gradient GEMMs hand the norm their sums of
+            # squares (no second pass over the fp32 gradient at step end)
+            elif comm.get("fused_grad_norm", True) and hasattr(self.buffer, "enable_fused_norm") \
+                    and getattr(self.optimizer, "grad_clip", None) is not None:
+                self.buffer.enable_fused_norm()
             # ZeRO-1/2: the post-update parameter all-gather hides under the next forward
             if comm.get("overlap_param_gather", True) and not self._pipeline \
                     and hasattr(self.buffer, "enable_param_gather_overlap"):

@@ -110,10 +110,18 @@ def _ok(*ts):
 
 
 def _launch(dt, la, lb, epi, M, N, K, A, lda, B, ldb, C, ldc, bias=None, aux=None, ldaux=0,
-            beta=0):
+            beta=0, sq=None):
     return _lib.kernels().gemm(dt, la, lb, epi, M, N, K, A.data_ptr(), lda, B.data_ptr(), ldb,
                                C.data_ptr(), ldc, _lib.ptr(bias), _lib.ptr(aux), ldaux, int(beta),
-                               _lib.stream())
+                               _lib.stream(), _lib.ptr(sq))
+
+
+def sq_slots(n, k):
+    """fp32 slots :func:`linear_wgrad` may write with ``sq`` for an [n, k]
+    weight gradient: one per wave of every 128 x 128 tile (the 256-tile
+    geometry uses the first quarter; slots it does not write keep their
+    zero)."""
+    return 4 * ((n + 127) // 128) * ((k + 127) // 128)
 
 
 def linear_fwd(x2, w, bias=None, act=None, out=None):
@@ -176,8 +184,14 @@ def covers_wgrad(dy2, x2):
         and x2.shape[1] >= 8
 
 
-def linear_wgrad(dy2, x2, out32, accumulate):
-    """``out32[N,K] (+)= dy2[M,N]^T @ x2[M,K]`` in fp32.  Returns True if done."""
+def linear_wgrad(dy2, x2, out32, accumulate, sq=None):
+    """``out32[N,K] (+)= dy2[M,N]^T @ x2[M,K]`` in fp32.  Returns True if done.
+
+    ``sq`` (fp32, :func:`sq_slots` long): the epilogue also writes the sums of
+    squares of the values it stores, so the global gradient norm needs no
+    second pass over this weight's gradient (parallel/grad_buffer.py,
+    ``enable_fused_norm``).  Returns False when the kernel cannot (the caller
+    then computes without it)."""
     if not enabled() or not _ok(dy2, x2) or dy2.dtype != x2.dtype:
         return False
     if out32.dtype != torch.float32 or not out32.is_contiguous():
@@ -187,8 +201,10 @@ def linear_wgrad(dy2, x2, out32, accumulate):
     if out32.shape != (N, K):
         raise ValueError("linear_wgrad: out shape {} != {}".format(tuple(out32.shape), (N, K)))
     # C[N, K] = sum_m A[n, m] B[m, k]: A = dy stored [m][n], B = x stored [m][k]
+    if sq is not None and (sq.dtype != torch.float32 or sq.numel() < sq_slots(N, K)):
+        raise ValueError("linear_wgrad: sq needs {} fp32 slots".format(sq_slots(N, K)))
     rc = _launch(_lib.dt_code(dy2.dtype), LAY_MC, LAY_MC, EPI_F32, N, K, M, dy2, dy2.stride(0),
-                 x2, x2.stride(0), out32, K, beta=accumulate)
+                 x2, x2.stride(0), out32, K, beta=accumulate, sq=sq)
     if rc == 0:
         _lib.maybe_sync()
     return rc == 0

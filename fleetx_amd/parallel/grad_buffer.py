@@ -177,6 +177,7 @@ class FlatParamGradBuffer:
         self._accumulating = True
         self._last_micro = True
         self._norm_stream = None
+        self._fused_norm = None
         self.early_norm = None
         self._install_hooks()
 
@@ -216,6 +217,7 @@ class FlatParamGradBuffer:
             else:
                 param.main_grad.add_(g)
             param._fx_fresh = False
+            param._fx_sq_ok = False  # this write left no norm partials
             param.grad = None
             grad_part_done(param)
         return hook
@@ -279,6 +281,75 @@ class FlatParamGradBuffer:
         part = self._norm_part
         self.early_norm = (part[self._norm_dist_idx].sum(), part[self._norm_rep_idx].sum())
 
+    # ------------------------------------------------------------------ fused grad norm
+    def enable_fused_norm(self):
+        """Gradient-norm partials from the weight-gradient GEMM's epilogue.
+
+        Every fused-wgrad matrix gets a region of fp32 slots that the
+        hand-written GEMM's fp32 epilogue fills with sums of squares of the
+        values it writes into ``main_grad`` (``ops.gemm.linear_wgrad(sq=)``;
+        later micro-batches overwrite them with the accumulated values).  At
+        ``finish()`` the norm is the sum of those slots plus one sum-of-squares
+        pass over whatever they do not cover (embeddings, biases, norms, any
+        weight whose gradient took another path this step) -- instead of
+        re-reading the whole fp32 gradient (27 GB, 4.7 ms for 6.7B on one
+        MI355X).  Single data rank only (with data parallel / ZeRO the norm is
+        over reduced gradients); mutually exclusive with ``enable_early_norm``."""
+        if self.device.type != "cuda" or self.dp_group is not None or \
+                self.shard_group is not None or self._norm_stream is not None:
+            return False
+        if self.mp_group is not None and any(c.seq_parallel for c in self.categories):
+            return False
+        from ..ops import gemm as G
+        self._fused_norm = {}
+        for c in self.categories:
+            if c.norm_excluded or c.seq_parallel:
+                continue
+            elig = [p for n, p in c.params if p.dim() == 2 and p._fx_fused_wgrad
+                    and getattr(p, "_fx_gemm_wgrad", False)
+                    and getattr(p, "_fx_grad_parts", 1) == 1]
+            if not elig:
+                continue
+            sizes = [G.sq_slots(*p.shape) for p in elig]
+            slots = torch.zeros(sum(sizes), dtype=torch.float32, device=self.device)
+            o = 0
+            for p, k in zip(elig, sizes):
+                p._fx_sq = slots[o:o + k]
+                p._fx_sq_ok = False
+                o += k
+            self._fused_norm[id(c)] = (slots, elig)
+        return True
+
+    def _finish_fused_norm(self):
+        from ..optims.optimizer import _sumsq
+        dist_parts, rep_parts = [], []
+        for c in self.categories:
+            if c.norm_excluded:
+                continue
+            parts = dist_parts if c.distributed else rep_parts
+            slots, elig = self._fused_norm.get(id(c), (None, ()))
+            ok = {id(p) for p in elig if p._fx_sq_ok}
+            if slots is not None and len(ok) == len(elig):
+                parts.append(slots.sum())
+            else:
+                parts += [p._fx_sq.sum() for p in elig if id(p) in ok]
+            seg = None  # contiguous runs of uncovered parameters (padding is zero)
+            for n, p in c.params:
+                o, k = self.offsets[id(p)]
+                if id(p) in ok:
+                    if seg is not None:
+                        parts.append(_sumsq(self.grad_flat[seg[0]:seg[1]]))
+                        seg = None
+                elif seg is None:
+                    seg = [o, o + k]
+                else:
+                    seg[1] = o + k
+            if seg is not None:
+                parts.append(_sumsq(self.grad_flat[seg[0]:seg[1]]))
+        zero = torch.zeros((), dtype=torch.float32, device=self.device)
+        self.early_norm = (torch.stack(dist_parts).sum() if dist_parts else zero,
+                           torch.stack(rep_parts).sum() if rep_parts else zero)
+
     def _data_groups(self):
         return self.dp_group, self.shard_group
 
@@ -327,6 +398,7 @@ class FlatParamGradBuffer:
             if p._fx_fresh:  # no gradient this step
                 p.main_grad.zero_()
                 p._fx_fresh = False
+                p._fx_sq_ok = False
         for b in self.buckets:
             if not b.launched:
                 self._launch(b)
@@ -357,6 +429,8 @@ class FlatParamGradBuffer:
                     dist.all_reduce(p.main_grad, group=self.embed_group.group)
         if self._norm_stream is not None:
             self._finish_early_norm()
+        elif self._fused_norm is not None:
+            self._finish_fused_norm()
         for b in self.buckets:
             b.launched = False
             b.work = None

@@ -97,6 +97,7 @@ class ColumnParallelLinear(nn.Module):
                                                         device=device))
         self.weight.tp_split = t > 1
         self.weight._fx_fused_wgrad_ok = True
+        self.weight._fx_gemm_wgrad = True  # gradient from the wgrad GEMM (fused-norm partials)
         if bias:
             self.bias = nn.Parameter(init_full_then_slice((out_features,), 0.0, name + ".bias",
                                                           dim=0, dtype=dtype, device=device,
@@ -145,6 +146,7 @@ class RowParallelLinear(nn.Module):
                                                         device=device))
         self.weight.tp_split = t > 1
         self.weight._fx_fused_wgrad_ok = True
+        self.weight._fx_gemm_wgrad = True  # gradient from the wgrad GEMM (fused-norm partials)
         if bias:
             self.bias = nn.Parameter(init_full_then_slice((out_features,), 0.0, name + ".bias",
                                                           dtype=dtype, device=device,

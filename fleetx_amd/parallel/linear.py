@@ -143,7 +143,21 @@ def accumulate_wgrad(weight, dy2, x2, bias=None, notify=True):
 def _accumulate_wgrad(weight, dy2, x2, bias=None, notify=True, bias_notify=True):
     mg = weight.main_grad
     fresh = getattr(weight, "_fx_fresh", False)
-    if G.use("wgrad", dy2, x2) and G.linear_wgrad(dy2, x2, mg, not fresh):
+    # gradient-norm partials from the epilogue (grad_buffer.enable_fused_norm):
+    # valid only while EVERY write of this step's gradient produced them
+    sq = getattr(weight, "_fx_sq", None)
+    done = False
+    if G.use("wgrad", dy2, x2):
+        if sq is not None and (fresh or weight._fx_sq_ok):
+            done = G.linear_wgrad(dy2, x2, mg, not fresh, sq=sq)
+            weight._fx_sq_ok = done
+        if not done:
+            if sq is not None:
+                weight._fx_sq_ok = False
+            done = G.linear_wgrad(dy2, x2, mg, not fresh)
+    elif sq is not None:
+        weight._fx_sq_ok = False
+    if done:
         db = None
         if bias is not None:
             if _fused(bias):

@@ -112,6 +112,28 @@ def test_wgrad_f32(gemm, M, N, K, dtype):
     assert _rel(out, ref + base) < 1e-4
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 768, 512), (2048, 1000, 256), (256, 4096, 4096)])
+def test_wgrad_norm_partials(gemm, M, N, K):
+    # the fp32 epilogue's per-wave sums of squares add up to |out|^2 of the
+    # values it stored, for beta 0 and beta 1; slots it does not own stay 0
+    # ((256, 4096, 4096) runs the 256-tile geometry, the others 128-tiles)
+    torch.manual_seed(5)
+    dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    out = torch.randn(N, K, device="cuda", dtype=torch.float32)
+    sq = torch.zeros(gemm.sq_slots(N, K) + 16, device="cuda")
+    sq[-16:] = 7.0  # guard: never written
+    assert gemm.linear_wgrad(dy, x, out, True, sq=sq[:-16])
+    ref = out.double().pow(2).sum()
+    assert abs(float(sq[:-16].double().sum()) - float(ref)) < 1e-5 * float(ref)
+    assert torch.all(sq[-16:] == 7.0)
+    assert gemm.linear_wgrad(dy, x, out, False, sq=sq[:-16])
+    ref = out.double().pow(2).sum()
+    assert abs(float(sq[:-16].double().sum()) - float(ref)) < 1e-5 * float(ref)
+    with pytest.raises(ValueError):
+        gemm.linear_wgrad(dy, x, out, False, sq=sq[:8])
+
+
 def test_strided_rows(gemm):
     """Row-strided activations (a column slice of a wider buffer) are read in place."""
     torch.manual_seed(5)
