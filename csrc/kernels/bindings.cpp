@@ -35,6 +35,7 @@ void fx_ce_bwd(int, const void*, void*, const int64_t*, const float*, const floa
                int, hipStream_t);
 int fx_sumsq_blocks(long n);
 void fx_sumsq_f32(const float*, long, float*, int, hipStream_t);
+void fx_sumsq_chunks(const int64_t*, const int64_t*, int, float*, hipStream_t);
 void fx_adamw_tune(int, int, int);
 void fx_adamw_flat(int, float*, const float*, float*, float*, void*, long, float, float, float,
                    float, float, float, const float*, const int*, const int*, hipStream_t);
@@ -154,6 +155,10 @@ PYBIND11_MODULE(_kernels, m) {
               V, vstart, ignore, S(st));
   });
   m.def("sumsq_blocks", &fx_sumsq_blocks);
+  m.def("sumsq_chunks", [](ptr addr, ptr len, int n, ptr partial, ptr st) {
+    fx_sumsq_chunks(reinterpret_cast<const int64_t*>(addr), reinterpret_cast<const int64_t*>(len),
+                    n, F(partial), S(st));
+  });
   m.def("sumsq_f32", [](ptr x, long n, ptr partial, int blocks, ptr st) {
     fx_sumsq_f32(F(x), n, F(partial), blocks, S(st));
   });

@@ -110,6 +110,39 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const uint16_t* __restrict_
 }
 
 // --------------------------------------------------------------- norms
+// Segmented sum of squares: block b reduces fp32 chunk b = (address, length),
+// any number of separate tensors in ONE launch (the fused gradient norm's
+// epilogue slots plus the gradient ranges they do not cover).  A negative
+// length -n marks a chunk that already holds sums of squares (epilogue
+// slots): its n values are added, not squared.
+__global__ __launch_bounds__(256) void sumsq_chunks_kernel(const int64_t* __restrict__ addr,
+                                                           const int64_t* __restrict__ len,
+                                                           float* __restrict__ partial) {
+  const float* x = reinterpret_cast<const float*>(addr[blockIdx.x]);
+  const long l = len[blockIdx.x];
+  const bool plain = l < 0;
+  const long n = plain ? -l : l;
+  float s = 0.f;
+  if (plain) {
+    for (long i = threadIdx.x; i < n; i += 256) s += x[i];
+  } else if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    const long n4 = n / 4;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    for (long i = threadIdx.x; i < n4; i += 256) {
+      const float4 v = x4[i];
+      s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+    for (long i = n4 * 4 + threadIdx.x; i < n; i += 256) s += x[i] * x[i];
+  } else {
+    for (long i = threadIdx.x; i < n; i += 256) s += x[i] * x[i];
+  }
+  __shared__ float red[4];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
 // partial[block] = sum of squares over a grid-stride slice (fp32 input)
 __global__ __launch_bounds__(256) void sumsq_f32_kernel(const float* __restrict__ x, long n,
                                                         float* __restrict__ partial) {
@@ -357,6 +390,11 @@ extern "C" void fx_ce_bwd(int dtype, const void* logits, void* dx, const int64_t
 }
 
 extern "C" int fx_sumsq_blocks(long n) { return grid_n(n / 4 + 1, 256) > 1024 ? 1024 : grid_n(n / 4 + 1, 256); }
+
+extern "C" void fx_sumsq_chunks(const int64_t* addr, const int64_t* len, int nchunks,
+                                float* partial, hipStream_t st) {
+  if (nchunks > 0) sumsq_chunks_kernel<<<nchunks, 256, 0, st>>>(addr, len, partial);
+}
 
 extern "C" void fx_sumsq_f32(const float* x, long n, float* partial, int blocks, hipStream_t st) {
   sumsq_f32_kernel<<<blocks, 256, 0, st>>>(x, n, partial);

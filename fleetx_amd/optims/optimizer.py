@@ -290,18 +290,34 @@ class FusedAdamW(FlatOptimizer):
         wide = int(os.environ.get("FLEETX_ADAMW_OVERLAP_WIDE", str(int(self.overlap_wide))))
         if grid:
             k.adamw_tune(grid, 1, wide)
-        with torch.cuda.stream(os_):
-            st = _lib.stream()
+        if getattr(self, "_overlap_args", None) is None:
+            # launch arguments per unit, built once (the flat buffers never
+            # move): the per-step host cost is then one bound call per range
+            # -- on the 1.3B model slicing every view each step kept the GPU
+            # waiting ~1.5 ms per step for the next forward
+            units = []
             for u, pieces in self._overlap_groups:
+                args = []
                 for ri, lo, hi in pieces:
                     s, e, c = self.ranges[ri]
-                    wd = self.weight_decay if c.decay else 0.0
                     a, b = lo - s, hi - s
-                    k.adamw_flat(dt, self.master[ri][a:b].data_ptr(), gf[lo:hi].data_ptr(),
+                    args.append((self.master[ri][a:b].data_ptr(), gf[lo:hi].data_ptr(),
                                  self.m[ri][a:b].data_ptr(), self.v[ri][a:b].data_ptr(),
-                                 pf[lo:hi].data_ptr(), hi - lo, float(lr), self.beta1, self.beta2,
-                                 self.eps, float(wd), 0.0, self.gscale.data_ptr(),
-                                 self.found_inf.data_ptr(), self.dev_step.data_ptr(), st)
+                                 pf[lo:hi].data_ptr(), hi - lo,
+                                 float(self.weight_decay if c.decay else 0.0)))
+                units.append((u, args))
+            self._overlap_args = units
+            self._overlap_dev = (self.gscale.data_ptr(), self.found_inf.data_ptr(),
+                                 self.dev_step.data_ptr())
+        gs, fi, ds = self._overlap_dev
+        lr = float(lr)
+        adamw = k.adamw_flat
+        b1, b2, eps = self.beta1, self.beta2, self.eps
+        with torch.cuda.stream(os_):
+            st = _lib.stream()
+            for u, args in self._overlap_args:
+                for mp, gp, m1, v1, pp, n, wd in args:
+                    adamw(dt, mp, gp, m1, v1, pp, n, lr, b1, b2, eps, wd, 0.0, gs, fi, ds, st)
                 ev = torch.cuda.Event()
                 ev.record(os_)
                 self._unit_events[u] = ev

@@ -320,35 +320,66 @@ class FlatParamGradBuffer:
             self._fused_norm[id(c)] = (slots, elig)
         return True
 
-    def _finish_fused_norm(self):
-        from ..optims.optimizer import _sumsq
-        dist_parts, rep_parts = [], []
+    _NORM_CHUNK = 1 << 18  # fp32 elements per block of the segmented sum of squares
+
+    def _fused_norm_plan(self, okey):
+        """(addr, len, n_dist) device tensors for one segmented sum-of-squares
+        launch: the epilogue slots of covered weights and the gradient ranges
+        of everything else, split into chunks, distributed (mp-sharded)
+        chunks first."""
+        chunks = {True: [], False: []}
+
+        def add(t_addr, n, dist_, squared=False):
+            # squared: the values are already sums of squares (epilogue slots)
+            for o in range(0, n, self._NORM_CHUNK):
+                m = min(self._NORM_CHUNK, n - o)
+                chunks[dist_].append((t_addr + 4 * o, -m if squared else m))
+
+        base = self.grad_flat.data_ptr()
         for c in self.categories:
             if c.norm_excluded:
                 continue
-            parts = dist_parts if c.distributed else rep_parts
             slots, elig = self._fused_norm.get(id(c), (None, ()))
             ok = {id(p) for p in elig if p._fx_sq_ok}
             if slots is not None and len(ok) == len(elig):
-                parts.append(slots.sum())
+                add(slots.data_ptr(), slots.numel(), c.distributed, squared=True)
             else:
-                parts += [p._fx_sq.sum() for p in elig if id(p) in ok]
+                for p in elig:
+                    if id(p) in ok:
+                        add(p._fx_sq.data_ptr(), p._fx_sq.numel(), c.distributed, squared=True)
             seg = None  # contiguous runs of uncovered parameters (padding is zero)
             for n, p in c.params:
                 o, k = self.offsets[id(p)]
                 if id(p) in ok:
                     if seg is not None:
-                        parts.append(_sumsq(self.grad_flat[seg[0]:seg[1]]))
+                        add(base + 4 * seg[0], seg[1] - seg[0], c.distributed)
                         seg = None
                 elif seg is None:
                     seg = [o, o + k]
                 else:
                     seg[1] = o + k
             if seg is not None:
-                parts.append(_sumsq(self.grad_flat[seg[0]:seg[1]]))
+                add(base + 4 * seg[0], seg[1] - seg[0], c.distributed)
+        allc = chunks[True] + chunks[False]
+        addr = torch.tensor([a for a, _ in allc] or [0], dtype=torch.int64, device=self.device)
+        lens = torch.tensor([n for _, n in allc] or [0], dtype=torch.int64, device=self.device)
+        return addr, lens, len(allc), len(chunks[True])
+
+    def _finish_fused_norm(self):
+        from ..ops import _lib
+        okey = tuple(p._fx_sq_ok for slots, elig in self._fused_norm.values() for p in elig)
+        cache = self.__dict__.setdefault("_norm_plans", {})
+        plan = cache.get(okey)
+        if plan is None:
+            plan = cache[okey] = self._fused_norm_plan(okey)
+        addr, lens, nch, nd = plan
+        part = torch.empty(max(nch, 1), dtype=torch.float32, device=self.device)
+        if nch:
+            _lib.kernels().sumsq_chunks(addr.data_ptr(), lens.data_ptr(), nch, part.data_ptr(),
+                                        _lib.stream())
         zero = torch.zeros((), dtype=torch.float32, device=self.device)
-        self.early_norm = (torch.stack(dist_parts).sum() if dist_parts else zero,
-                           torch.stack(rep_parts).sum() if rep_parts else zero)
+        self.early_norm = (part[:nd].sum() if nd else zero,
+                           part[nd:nch].sum() if nch > nd else zero)
 
     def _data_groups(self):
         return self.dp_group, self.shard_group
