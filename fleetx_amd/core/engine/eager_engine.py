@@ -170,6 +170,8 @@ class EagerEngine(BasicEngine):
             self._dtype = torch.float32  # reference: pure fp16 disabled for export
         model.to(self._dtype)
         self._pipeline = hasattr(model, "train_batch")
+        self._fused_head = bool(getattr(getattr(model, "cfg", None), "fused_lm_head_ce", False)) \
+            and not self._pipeline
 
         self.buffer, self.optimizer, self.lr_scheduler = None, optimizer, lr
         self.scaler = None
@@ -329,6 +331,7 @@ class EagerEngine(BasicEngine):
         loss = None
         for i, mb in enumerate(micro):
             self.buffer.set_last_micro_batch(i == len(micro) - 1)
+            self._declare_head_grad()
             l = self._module.training_step(mb)
             if self._accumulate_steps > 1:
                 l = l / self._accumulate_steps
@@ -400,6 +403,7 @@ class EagerEngine(BasicEngine):
             for i, mb in enumerate(micro):
                 self.buffer.set_last_micro_batch(i == len(micro) - 1)
                 with phase("Forward"):
+                    self._declare_head_grad()
                     l = self._module.training_step(mb)
                     if self._accumulate_steps > 1:
                         l = l / self._accumulate_steps
@@ -411,6 +415,16 @@ class EagerEngine(BasicEngine):
         with phase("Optimization"):
             self._optim_update()
         return loss
+
+    def _declare_head_grad(self):
+        """Fused LM-head cross-entropy (``Model.fused_lm_head_ce``): the head's
+        backward runs inside the forward, so the gradient the loss will
+        receive -- 1 / accumulation steps x the fp16 loss scale -- is
+        declared before each micro-batch (ops/lm_head_ce.py)."""
+        if self._fused_head:
+            from ...ops import lm_head_ce
+            lm_head_ce.declare_grad_scale(self.scaler.scale if self.scaler is not None else None,
+                                          self._accumulate_steps)
 
     def _optim_update(self):
         self.optimizer.step()
@@ -478,6 +492,9 @@ class EagerEngine(BasicEngine):
                     # a one-shot all-reduce that timed out on a peer wrote NaN
                     # and flagged it: stop here, naming the group
                     _comm.check_all()
+                if self._fused_head:
+                    from ...ops import lm_head_ce
+                    lm_head_ce.check()
                 cost = (time.time() - t0) / self._logging_freq
                 lval = self._reduce_log_loss(loss_acc, n_acc)
                 if self._nan_guard != "off" and not np.isfinite(lval):

@@ -41,7 +41,7 @@ class GPTConfig:
                  max_position_embeddings=1024, type_vocab_size=16, initializer_range=0.02,
                  use_recompute=False, recompute_granularity=None, sequence_parallel=False,
                  layer_norm_eps=1e-5, fused_linear=False, no_recompute_layers=None,
-                 dtype=torch.float32, **unused):
+                 fused_lm_head_ce=False, dtype=torch.float32, **unused):
         self.vocab_size = vocab_size
         self.hidden_size = hidden_size
         self.num_layers = num_layers
@@ -59,13 +59,15 @@ class GPTConfig:
         self.no_recompute_layers = set(no_recompute_layers or [])
         self.dtype = dtype
         self.head_dim = hidden_size // num_attention_heads
+        # training: LM head + CE chunked over tokens, logits never whole (ops/lm_head_ce.py)
+        self.fused_lm_head_ce = bool(fused_lm_head_ce)
 
     @classmethod
     def from_model_config(cls, cfg, dtype=torch.float32):
         keys = ["vocab_size", "hidden_size", "num_layers", "num_attention_heads", "ffn_hidden_size",
                 "hidden_dropout_prob", "attention_probs_dropout_prob", "max_position_embeddings",
                 "type_vocab_size", "initializer_range", "use_recompute", "recompute_granularity",
-                "sequence_parallel", "no_recompute_layers", "layer_norm_eps"]
+                "sequence_parallel", "no_recompute_layers", "layer_norm_eps", "fused_lm_head_ce"]
         kw = {k: cfg[k] for k in keys if k in cfg and cfg[k] is not None}
         return cls(dtype=dtype, **kw)
 
@@ -261,8 +263,11 @@ class GPTForPretraining(nn.Module):
 
     def forward(self, input_ids, position_ids=None):
         h = self.gpt(input_ids, position_ids)
-        logits = L.parallel_lm_logits(h, self.gpt.embeddings.word_embeddings.weight,
-                                      parallel_output=True,
+        w = self.gpt.embeddings.word_embeddings.weight
+        if self.cfg.fused_lm_head_ce and self.training:
+            # the criterion runs head + CE chunk by chunk (ops/lm_head_ce.py)
+            return L.parallel_lm_head_input(h, w, sequence_parallel=self.cfg.sequence_parallel)
+        logits = L.parallel_lm_logits(h, w, parallel_output=True,
                                       sequence_parallel=self.cfg.sequence_parallel)
         return logits  # [b, s, V/t], or [s, b, V/t] under sequence parallelism
 
@@ -278,6 +283,16 @@ class GPTPretrainingCriterion(nn.Module):
         if self.seq_first:
             labels, loss_mask = labels.t(), loss_mask.t()
         g = topo.get_hcg().get_model_parallel_group()
+        if isinstance(logits, L.HeadInput):
+            from ....parallel.linear import linear
+            from ....ops import lm_head_ce
+            hi = logits
+            vocab_start = topo.mp_rank() * hi.weight.shape[0]
+            if lm_head_ce.supported(hi.h2, hi.weight):
+                return lm_head_ce.lm_head_cross_entropy(
+                    hi.h2, hi.weight, labels.reshape(-1), loss_mask.reshape(-1),
+                    group=g if g.nranks > 1 else None, vocab_start=vocab_start)
+            logits = linear(hi.h2, hi.weight)  # no flat grad buffer: the plain head
         vocab_start = topo.mp_rank() * logits.shape[-1]
         ce = ops.softmax_cross_entropy(logits, labels, group=g if g.nranks > 1 else None,
                                        vocab_start=vocab_start)

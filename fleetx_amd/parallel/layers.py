@@ -208,6 +208,27 @@ def parallel_lm_logits(h, weight, parallel_output=True, sequence_parallel=False)
     return logits
 
 
+class HeadInput:
+    """What the GPT model hands its criterion when the LM head and the
+    cross-entropy run fused and chunked (``ops/lm_head_ce.py``): the hidden
+    states after the mp copy / sequence gather as ``[tokens, h]`` (token
+    order = the logits' row order), and the tied vocab-shard weight."""
+    __slots__ = ("h2", "weight")
+
+    def __init__(self, h2, weight):
+        self.h2, self.weight = h2, weight
+
+
+def parallel_lm_head_input(h, weight, sequence_parallel=False):
+    """The input half of :func:`parallel_lm_logits`: ``h`` prepared exactly as
+    for the head GEMM, which the criterion then runs chunk by chunk."""
+    if sequence_parallel:
+        h = M.all_gather_seq(h)
+    else:
+        h = M.copy_to_mp(h)
+    return HeadInput(h.reshape(-1, h.shape[-1]), weight)
+
+
 def mark_sequence_parallel(module):
     """Tag replicated params (LN, row-bias) whose grads need an mp all-reduce."""
     for p in module.parameters():

@@ -253,3 +253,13 @@ def test_fingerprint_mode_trains_identically(ref_losses, layout):
     world = layout[0] * layout[1] * layout[2] * layout[3]
     _check(dist_utils.run(_train, world, layout, 3, ("Distributed.debug=fingerprint",)),
            ref_losses)
+
+
+@pytest.mark.parametrize("layout", [(1, 2, 1, 1, 0, GBS, False, 1), (1, 2, 1, 1, 0, GBS, True, 1),
+                                    (2, 1, 1, 1, 0, 2, False, 1)])
+def test_fused_lm_head_ce(ref_losses, layout, monkeypatch):
+    """LM head + CE chunked over tokens (ops/lm_head_ce.py) on a vocab-parallel
+    head (TP2, TP2 + SP) and under DP with accumulation: the plain head's
+    loss curve."""
+    monkeypatch.setenv("FLEETX_LM_HEAD_CE_CHUNK", "48")
+    _check(dist_utils.run(_train, 2, layout, 3, ("Model.fused_lm_head_ce=True",)), ref_losses)

@@ -159,3 +159,28 @@ def test_profiler_views(tmp_path):
     for ph in ("Dataloader", "Forward", "Backward", "GradSync", "Optimization"):
         assert ph in text.split("Model Summary")[1].split("Kernel Summary")[0], text
     assert any(p.name.startswith("trace_rank0") for p in (tmp_path / "prof").iterdir())
+
+
+@pytest.mark.parametrize("micro", [4, 2])
+def test_fused_lm_head_ce_matches_plain_head(tmp_path, micro, monkeypatch):
+    """ops/lm_head_ce.py: head + CE chunked over tokens (3 chunks of 48 rows
+    over 128 tokens, the last one short) with the head's backward inside the
+    forward -- same losses and same trained weights as the plain head, with
+    and without gradient accumulation (declared upstream gradient 1/2)."""
+    monkeypatch.setenv("FLEETX_LM_HEAD_CE_CHUNK", "48")
+    runs = []
+    for fused in (False, True):
+        e, _ = _engine(tmp_path / str(fused), ["Global.micro_batch_size=%d" % micro,
+                                               "Model.fused_lm_head_ce=%s" % fused,
+                                               "Model.hidden_dropout_prob=0.0",
+                                               "Model.attention_probs_dropout_prob=0.0"])
+        assert e._fused_head == fused
+        losses = [float(e._fit_impl(_batch(i))) for i in range(3)]
+        e.optimizer.sync_state()
+        runs.append((losses, e.buffer.param_flat.clone()))
+    (l0, p0), (l1, p1) = runs
+    for a, b in zip(l0, l1):
+        assert abs(a - b) < 1e-5 * abs(b), (l0, l1)
+    assert torch.allclose(p0, p1, rtol=1e-5, atol=1e-6), float((p0 - p1).abs().max())
+    from fleetx_amd.ops import lm_head_ce
+    lm_head_ce.check()  # the declared gradient matched every backward

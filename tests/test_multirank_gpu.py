@@ -169,3 +169,17 @@ def test_tp_oneshot_allreduce_matches_single_rank(ref_gpu, name):
     out = dist_utils.run(_train_gpu_oneshot, 2, LAYOUTS[name], timeout=300)
     assert all(r["oneshot_calls"] > 0 for r in out), [r["oneshot_calls"] for r in out]
     _check(out, ref_gpu)
+
+
+def _train_gpu_fused_head(rank, world, layout):
+    # LM head + CE chunked over tokens (ops/lm_head_ce.py): 4 chunks per rank
+    os.environ["FLEETX_LM_HEAD_CE_CHUNK"] = "256"
+    return _train_gpu(rank, world, layout, extra=("Model.fused_lm_head_ce=True",))
+
+
+@pytest.mark.parametrize("name", ["single", "tp2", "tp2_sp"])
+def test_fused_lm_head_ce_matches_single_rank(ref_gpu, name):
+    layout = dict(LAYOUTS, single=(1, 1, 1, 1, 0, GBS, False, 1))[name]
+    out = dist_utils.run(_train_gpu_fused_head, 1 if name == "single" else 2, layout,
+                         timeout=300)
+    _check(out, ref_gpu)
