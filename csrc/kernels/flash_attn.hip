@@ -292,6 +292,111 @@ __device__ __forceinline__ void lpt_order(int lid, int nper, int BH, int& bh, in
   bh = c * G + j % Gc;
 }
 
+// One 64-key tile of the forward for this wave's 32 queries: S^T = K.Q^T,
+// online softmax (mask on diagonal / tail tiles, deferred rescale, dropout on
+// P), O^T += V^T.P^T.  Shared by the per-block and the persistent kernels.
+template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
+__device__ __forceinline__ void fwd_tile(const AttnParams& P, const Frag<D>& F, const char* kt,
+                                         const char* vt, const short8 (&qf)[D / 16],
+                                         floatx16 (&oacc)[D / 32], float& m_run, float& lsum,
+                                         int kb, int wq0, int qi, int kv_len, int b, int h,
+                                         float sl2, uint32_t cb) {
+  constexpr int KV = 64;
+  // waves without a valid query (the tail block of S = 257) only help load
+  if (wq0 < P.Sq && !(CAUSAL && kb > wq0 + 31)) {
+    floatx16 sacc[2];
+    // all K fragments of the tile up front: the 16 LDS reads overlap each
+    // other instead of one exposed LDS latency per MFMA
+    short8 kfr[2][D / 16];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) kfr[t][s] = F.row(kt, t, s);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[t][i] = 0.f;
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) sacc[t] = mfma<T>(kfr[t][s], qf[s], sacc[t]);
+    }
+    const bool need_mask = (CAUSAL && kb + KV - 1 > wq0) || (kb + KV > kv_len);
+    if constexpr (KB) key_bias_add(sacc, P.kbias + (long)b * P.kb_b + kb, h, sl2);
+    // Online softmax on the lane's 32 scores.  Without a key bias the raw
+    // scores are maxed and the scale folds into one FMA before the exp2
+    // (scale > 0 commutes with max).  Only tiles on the causal diagonal or
+    // past kv_len run the per-element key index / compare / select pass
+    // (wave-uniform branch, masked scores set to -inf in place).
+    if (__builtin_expect(need_mask, 0)) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = kb + 32 * t + crow(i, h);
+          if ((CAUSAL && key > qi) || key >= kv_len) sacc[t][i] = -INFINITY;
+        }
+    }
+    {
+      float mloc = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mloc = fmaxf(mloc, sacc[t][i]);
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      if constexpr (!KB) mloc *= sl2;
+      // Deferred rescale: the running max moves (and O / l are rescaled)
+      // only when some row of the wave grew by more than FA_RESCALE_THR
+      // (log2 units) -- otherwise p = exp2(s - m_run) stays <= 2^THR, exact
+      // in fp32 and as bf16 operands (same relative precision).  The
+      // decision precedes this tile's exp2, so O, l and P always share one
+      // reference max (tests/test_kernels_gpu.py forces the branch mid-row).
+      if (__any(mloc > m_run + FA_RESCALE_THR)) {
+        const float m_new = fmaxf(m_run, mloc);
+        const float alpha = fexp2(m_run - ((m_new == -INFINITY) ? 0.f : m_new));
+        m_run = m_new;
+        lsum *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+      }
+      const float m_use = (m_run == -INFINITY) ? 0.f : m_run;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+          float p0, p1;
+          if constexpr (KB) {
+            p0 = fexp2(sacc[t][i] - m_use);
+            p1 = fexp2(sacc[t][i + 1] - m_use);
+          } else {
+            p0 = fexp2(__builtin_fmaf(sacc[t][i], sl2, -m_use));
+            p1 = fexp2(__builtin_fmaf(sacc[t][i + 1], sl2, -m_use));
+          }
+          lsum += p0 + p1;
+          if (DROP) {  // the keep scale 1/(1-p) is applied once, to O
+            const int key = kb + 32 * t + crow(i, h);  // even
+            const uint32_t hh = lowbias32((((uint32_t)qi) << 16 | ((uint32_t)key >> 1)) ^ cb);
+            p0 = ((hh & 0xffffu) >= P.thr) ? p0 : 0.f;
+            p1 = ((hh >> 16) >= P.thr) ? p1 : 0.f;
+          }
+          sacc[t][i] = p0;
+          sacc[t][i + 1] = p1;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        short8 pf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[j] = cvt16<T>(sacc[t][8 * ss + j]);
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt)
+          oacc[dt] = mfma<T>(F.tr(vt, t, ss, dt), pf, oacc[dt]);
+      }
+  }
+}
+
 // ============================================================================
 // forward: WG = 4 waves x 32 queries = 128 queries; KV tile = 64 keys
 // ============================================================================
@@ -366,99 +471,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
       vld.load((it + 1) * KV, smem + 2 * TB + (cur ^ 1) * TB, lane);
     }
     const int kb = it * KV;
-    // waves without a valid query (the tail block of S = 257) only help load
-    if (wq0 < P.Sq && !(CAUSAL && kb > wq0 + 31)) {
-      floatx16 sacc[2];
-      // all K fragments of the tile up front: the 16 LDS reads overlap each
-      // other instead of one exposed LDS latency per MFMA
-      short8 kfr[2][D / 16];
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int s = 0; s < D / 16; ++s) kfr[t][s] = F.row(kt, t, s);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sacc[t][i] = 0.f;
-#pragma unroll
-        for (int s = 0; s < D / 16; ++s) sacc[t] = mfma<T>(kfr[t][s], qf[s], sacc[t]);
-      }
-      const bool need_mask = (CAUSAL && kb + KV - 1 > wq0) || (kb + KV > kv_len);
-      if constexpr (KB) key_bias_add(sacc, P.kbias + (long)b * P.kb_b + kb, h, sl2);
-      // Online softmax on the lane's 32 scores.  Without a key bias the raw
-      // scores are maxed and the scale folds into one FMA before the exp2
-      // (scale > 0 commutes with max).  Only tiles on the causal diagonal or
-      // past kv_len run the per-element key index / compare / select pass
-      // (wave-uniform branch, masked scores set to -inf in place).
-      if (__builtin_expect(need_mask, 0)) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int key = kb + 32 * t + crow(i, h);
-            if ((CAUSAL && key > qi) || key >= kv_len) sacc[t][i] = -INFINITY;
-          }
-      }
-      {
-        float mloc = -INFINITY;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) mloc = fmaxf(mloc, sacc[t][i]);
-        mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-        if constexpr (!KB) mloc *= sl2;
-        // Deferred rescale: the running max moves (and O / l are rescaled)
-        // only when some row of the wave grew by more than FA_RESCALE_THR
-        // (log2 units) -- otherwise p = exp2(s - m_run) stays <= 2^THR, exact
-        // in fp32 and as bf16 operands (same relative precision).  The
-        // decision precedes this tile's exp2, so O, l and P always share one
-        // reference max (tests/test_kernels_gpu.py forces the branch mid-row).
-        if (__any(mloc > m_run + FA_RESCALE_THR)) {
-          const float m_new = fmaxf(m_run, mloc);
-          const float alpha = fexp2(m_run - ((m_new == -INFINITY) ? 0.f : m_new));
-          m_run = m_new;
-          lsum *= alpha;
-#pragma unroll
-          for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
-        }
-        const float m_use = (m_run == -INFINITY) ? 0.f : m_run;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int i = 0; i < 16; i += 2) {
-            float p0, p1;
-            if constexpr (KB) {
-              p0 = fexp2(sacc[t][i] - m_use);
-              p1 = fexp2(sacc[t][i + 1] - m_use);
-            } else {
-              p0 = fexp2(__builtin_fmaf(sacc[t][i], sl2, -m_use));
-              p1 = fexp2(__builtin_fmaf(sacc[t][i + 1], sl2, -m_use));
-            }
-            lsum += p0 + p1;
-            if (DROP) {  // the keep scale 1/(1-p) is applied once, to O
-              const int key = kb + 32 * t + crow(i, h);  // even
-              const uint32_t hh = lowbias32((((uint32_t)qi) << 16 | ((uint32_t)key >> 1)) ^ cb);
-              p0 = ((hh & 0xffffu) >= P.thr) ? p0 : 0.f;
-              p1 = ((hh >> 16) >= P.thr) ? p1 : 0.f;
-            }
-            sacc[t][i] = p0;
-            sacc[t][i + 1] = p1;
-          }
-      }
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          short8 pf;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) pf[j] = cvt16<T>(sacc[t][8 * ss + j]);
-#pragma unroll
-          for (int dt = 0; dt < D / 32; ++dt)
-            oacc[dt] = mfma<T>(F.tr(vt, t, ss, dt), pf, oacc[dt]);
-        }
-    }
+    fwd_tile<T, D, CAUSAL, DROP, KB>(P, F, kt, vt, qf, oacc, m_run, lsum, kb, wq0, qi, kv_len, b,
+                                     h, sl2, cb);
     glds_wait();
     __syncthreads();
   }
