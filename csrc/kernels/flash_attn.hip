@@ -294,7 +294,7 @@ __device__ __forceinline__ void lpt_order(int lid, int nper, int BH, int& bh, in
 
 // One 64-key tile of the forward for this wave's 32 queries: S^T = K.Q^T,
 // online softmax (mask on diagonal / tail tiles, deferred rescale, dropout on
-// P), O^T += V^T.P^T.  Shared by the per-block and the persistent kernels.
+// P), O^T += V^T.P^T.  (the per-block forward kernel).  
 template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
 __device__ __forceinline__ void fwd_tile(const AttnParams& P, const Frag<D>& F, const char* kt,
                                          const char* vt, const short8 (&qf)[D / 16],
