@@ -33,6 +33,8 @@ def timeit(fn, iters=200):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", type=int, nargs="+", default=[1, 16])
+    ap.add_argument("--warm", action="store_true",
+                    help="also time a weight resident in the Infinity Cache")
     args = ap.parse_args()
     from fleetx_amd.ops import gemm as G
     for name, (N, K) in SHAPES.items():
@@ -50,10 +52,18 @@ def main():
                 return ws[it[0]]
             us = timeit(lambda: G.decode_linear(x, nxt(), b))
             ub = timeit(lambda: F.linear(x, nxt(), b))
-            print(json.dumps({"shape": name, "M": M, "N": N, "K": K, 
-                              "gemv_us": round(us, 2), "gemv_TB_s": round(N * K * 2 / us / 1e6, 2),
-                              "hipblaslt_us": round(ub, 2),
-                              "hipblaslt_TB_s": round(N * K * 2 / ub / 1e6, 2)}), flush=True)
+            rec = {"shape": name, "M": M, "N": N, "K": K,
+                   "gemv_us": round(us, 2), "gemv_TB_s": round(N * K * 2 / us / 1e6, 2),
+                   "hipblaslt_us": round(ub, 2),
+                   "hipblaslt_TB_s": round(N * K * 2 / ub / 1e6, 2)}
+            if args.warm:
+                # the same weight every call: it stays in the 256 MB Infinity
+                # Cache (MALL) -- what a prefetch of the next GEMV's weights
+                # under the current phase would buy
+                w0 = ws[0]
+                uw = timeit(lambda: G.decode_linear(x, w0, b))
+                rec.update(gemv_warm_us=round(uw, 2), gemv_warm_TB_s=round(N * K * 2 / uw / 1e6, 2))
+            print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":
