@@ -722,10 +722,12 @@ __device__ __forceinline__ uint32_t dpp_swap1(uint32_t v) {
 // hash per query row, so each lane hashes every other query row and the
 // pair trades results through DPP (one hash per two elements, as fwd / dQ).
 // ============================================================================
-template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
-__global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int QT = FA_DKDV_QT, TB = QT * D * 2;
+// QT: query rows per tile (32, or 64 = half the barriers / DMA issue points
+// per unit of work); VREG: this wave's V rows in 32 VGPRs instead of a
+// 128-row LDS image (keeps two workgroups per CU at QT = 64).
+template <typename T, int D, bool CAUSAL, bool DROP, bool KB, int QT, bool VREG>
+__device__ __forceinline__ void dkdv_body(const AttnParams& P, char* smem) {
+  constexpr int TB = QT * D * 2;
   // one buffer: [Q tile][dO tile][lse2 QT floats][delta QT floats]; then V rows
   constexpr int BUF = 2 * TB + 2 * QT * 4;
   char* vs = smem + 2 * BUF;
@@ -763,8 +765,20 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
     else
       kf[s] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
   }
-  // V rows of this WG's 128 keys -> LDS (rows past Sk clamp; those keys are masked)
-  Glds<D, 128>::load(vp, P.sv_s, kblock * 128, P.Sk, vs, w, lane, P.dval);
+  // V rows of this WG's 128 keys -> LDS (rows past Sk clamp; those keys are
+  // masked), or this wave's 32 rows -> registers
+  short8 vf[VREG ? D / 16 : 1];
+  if constexpr (VREG) {
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      if (ki < P.Sk && 16 * s + 8 * h < P.dval)
+        vf[s] = *reinterpret_cast<const short8*>(vp + (long)ki * P.sv_s + 16 * s + 8 * h);
+      else
+        vf[s] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  } else {
+    Glds<D, 128>::load(vp, P.sv_s, kblock * 128, P.Sk, vs, w, lane, P.dval);
+  }
   floatx16 dkacc[D / 32], dvacc[D / 32];
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt)
@@ -820,7 +834,9 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
     const float* dl_s = lse_s + QT;
     // else: whole tile above this wave's keys, or the wave holds no valid key
     if (wk0 < P.Sk && !(CAUSAL && qb + QT - 1 < wk0)) {
-#pragma unroll
+      // one 32-query slice at a time (not interleaved by the compiler: the
+      // slices' fp32 tiles would not fit the 2-wave register budget together)
+#pragma unroll 1
       for (int t = 0; t < QT / 32; ++t) {
         const int q0 = qb + 32 * t;
         if (CAUSAL && q0 + 31 < wk0) continue;
@@ -858,7 +874,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
           sacc = mfma<T>(F.row(qt, t, s), kf[s], sacc);
-          dpacc = mfma<T>(F.row(gt, t, s), F.row(vs, w, s), dpacc);
+          if constexpr (VREG) dpacc = mfma<T>(F.row(gt, t, s), vf[s], dpacc);
+          else dpacc = mfma<T>(F.row(gt, t, s), F.row(vs, w, s), dpacc);
         }
         // P o Z (for dV) and dS (for dK) straight to bf16, one 8-row half at a
         // time: no fp32 copies of the tile stay live across the MFMAs
@@ -913,6 +930,17 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
           *reinterpret_cast<ushort4*>(dvp + dt * 32 + 8 * g + 4 * h) = c;
       }
   }
+}
+
+template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  dkdv_body<T, D, CAUSAL, DROP, KB, FA_DKDV_QT, false>(P, smem);
+}
+template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_q64v_kernel(AttnParams P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  dkdv_body<T, D, CAUSAL, DROP, KB, 64, true>(P, smem);
 }
 
 AttnParams make_params(const void* q, const void* k, const void* v, const long* qs,
@@ -1084,9 +1112,19 @@ static int flash_bwd_t(const void* q, const void* k, const void* v, const void* 
   {
     const int nk = (Sk + 127) / 128;
     // double-buffered Q/dO tiles + row constants, then the WG's V rows
-    const size_t smem = 2 * (2 * FA_DKDV_QT * D * 2 + 2 * FA_DKDV_QT * 4) + 128 * D * 2;
-    FA_DISPATCH(fa_bwd_dkdv_kernel, D, causal, p > 0.f, kbias != nullptr, nk * B * H, smem, st,
-                P);
+    // D <= 96: 64-query tiles with V in registers (bwd 0.150 -> 0.144 ms at
+    // B8 S1024 H16 D64, profiles/r3_dkdv/); D = 128 has no 32 VGPRs to spare.
+    // FLEETX_FA_DKDV=32 keeps 32-query tiles everywhere (A/B switch).
+    const char* e = getenv("FLEETX_FA_DKDV");
+    if (D <= 96 && (e == nullptr || atoi(e) != 32)) {
+      const size_t smem = 2 * (2 * 64 * D * 2 + 2 * 64 * 4);
+      FA_DISPATCH(fa_bwd_dkdv_q64v_kernel, D, causal, p > 0.f, kbias != nullptr, nk * B * H,
+                  smem, st, P);
+    } else {
+      const size_t smem = 2 * (2 * FA_DKDV_QT * D * 2 + 2 * FA_DKDV_QT * 4) + 128 * D * 2;
+      FA_DISPATCH(fa_bwd_dkdv_kernel, D, causal, p > 0.f, kbias != nullptr, nk * B * H, smem,
+                  st, P);
+    }
   }
   return 0;
 }
