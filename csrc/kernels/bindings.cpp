@@ -19,15 +19,16 @@ void fx_add_ln_fwd(int, const void*, const void*, const void*, const void*, cons
 void fx_ln_bwd_row(int, const void*, const void*, const float*, const float*, const void*,
                    const void*, void*, void*, int, int, float, uint64_t, hipStream_t);
 void fx_coltile_partial(int, int, const void*, const void*, const float*, const float*, float*,
-                        float*, int, int, int, hipStream_t);
+                        float*, int, int, int, hipStream_t, int*, float*, void*, int, float*,
+                        void*, int);
 void fx_coltile_finalize(int, const float*, int, int, float*, void*, int, hipStream_t);
 void fx_bias_gelu_fwd(int, int, const void*, const void*, void*, long, int, hipStream_t);
 void fx_bias_gelu_bwd(int, int, const void*, const void*, const void*, void*, float*, int, int, int,
-                      hipStream_t);
+                      hipStream_t, int*, float*, void*, int);
 void fx_bias_dropout_add_fwd(int, const void*, const void*, const void*, void*, long, int, float,
                              uint64_t, hipStream_t);
 void fx_dropout_bwd_colsum(int, const void*, void*, float*, int, int, int, float, uint64_t,
-                           hipStream_t);
+                           hipStream_t, int*, float*, void*, int);
 void fx_dropout_fwd(int, const void*, void*, long, float, uint64_t, hipStream_t);
 void fx_ce_stats(int, const void*, const int64_t*, int, int, long, float*, float*, float*, int,
                  hipStream_t);
@@ -79,6 +80,13 @@ void fx_gemm_set_variant(int);
 int fx_decode_gemv(int, int, int, int, int, const void*, long, const void*, long, const void*,
                    const void*, long, void*, long, void*, void*, const long*, int, int, int,
                    const void*, const void*, float, hipStream_t);
+int fx_decode_layer(int, int, int, int, int, int, int, int, const void*, void*, void*, float*,
+                    void*, void*, const void*, const void*, const void*, const void*, const void*,
+                    const void*, const void*, const void*, const void*, const void*, const void*,
+                    const void*, void*, void*, const long*, const int*, float, float, float,
+                    unsigned*, unsigned, int*, hipStream_t);
+int fx_decode_layer_grid();
+int fx_decode_layer_barriers();
 void fx_set_dropout_salt(const void*);
 void fx_set_adamw_lr_ptr(const void*);
 int fx_comm_max_world();
@@ -117,11 +125,19 @@ PYBIND11_MODULE(_kernels, m) {
     fx_ln_bwd_row(dt, CP(dy), CP(s), F(mean), F(rstd), CP(g), CP(ds_in), P(ds_out), P(dx_out),
                   rows, h, p, key, S(st));
   });
+  // column-sum producers: cnt != 0 fuses the finalize (last workgroup of a
+  // column tile sums the splits into f*/t* outputs); cnt == 0: the caller
+  // runs coltile_finalize
   m.def("coltile_partial", [](int dt, int mode, ptr a, ptr b, ptr mean, ptr rstd, ptr p0, ptr p1,
-                              int rows, int cols, int splits, ptr st) {
+                              int rows, int cols, int splits, ptr st, ptr cnt, ptr f0, ptr t0,
+                              int acc0, ptr f1, ptr t1, int acc1) {
     fx_coltile_partial(dt, mode, CP(a), CP(b), F(mean), F(rstd), F(p0), F(p1), rows, cols, splits,
-                       S(st));
-  });
+                       S(st), reinterpret_cast<int*>(cnt), F(f0), P(t0), acc0, F(f1), P(t1),
+                       acc1);
+  }, py::arg("dt"), py::arg("mode"), py::arg("a"), py::arg("b"), py::arg("mean"), py::arg("rstd"),
+     py::arg("p0"), py::arg("p1"), py::arg("rows"), py::arg("cols"), py::arg("splits"),
+     py::arg("st"), py::arg("cnt") = 0, py::arg("f0") = 0, py::arg("t0") = 0, py::arg("acc0") = 0,
+     py::arg("f1") = 0, py::arg("t1") = 0, py::arg("acc1") = 0);
   m.def("coltile_finalize", [](int dt, ptr part, int splits, int cols, ptr out_f32, ptr out_t,
                                int accumulate, ptr st) {
     fx_coltile_finalize(dt, F(part), splits, cols, F(out_f32), P(out_t), accumulate, S(st));
@@ -130,17 +146,25 @@ PYBIND11_MODULE(_kernels, m) {
     fx_bias_gelu_fwd(dt, erf, CP(x), CP(bias), P(y), n, cols, S(st));
   });
   m.def("bias_gelu_bwd", [](int dt, int erf, ptr dy, ptr x, ptr bias, ptr dx, ptr part, int rows,
-                            int cols, int splits, ptr st) {
-    fx_bias_gelu_bwd(dt, erf, CP(dy), CP(x), CP(bias), P(dx), F(part), rows, cols, splits, S(st));
-  });
+                            int cols, int splits, ptr st, ptr cnt, ptr out_f32, ptr out_t,
+                            int acc) {
+    fx_bias_gelu_bwd(dt, erf, CP(dy), CP(x), CP(bias), P(dx), F(part), rows, cols, splits, S(st),
+                     reinterpret_cast<int*>(cnt), F(out_f32), P(out_t), acc);
+  }, py::arg("dt"), py::arg("erf"), py::arg("dy"), py::arg("x"), py::arg("bias"), py::arg("dx"),
+     py::arg("part"), py::arg("rows"), py::arg("cols"), py::arg("splits"), py::arg("st"),
+     py::arg("cnt") = 0, py::arg("out_f32") = 0, py::arg("out_t") = 0, py::arg("acc") = 0);
   m.def("bias_dropout_add_fwd", [](int dt, ptr x, ptr bias, ptr res, ptr out, long n, int cols,
                                    float p, uint64_t key, ptr st) {
     fx_bias_dropout_add_fwd(dt, CP(x), CP(bias), CP(res), P(out), n, cols, p, key, S(st));
   });
   m.def("dropout_bwd_colsum", [](int dt, ptr dout, ptr dx, ptr part, int rows, int cols,
-                                 int splits, float p, uint64_t key, ptr st) {
-    fx_dropout_bwd_colsum(dt, CP(dout), P(dx), F(part), rows, cols, splits, p, key, S(st));
-  });
+                                 int splits, float p, uint64_t key, ptr st, ptr cnt, ptr out_f32,
+                                 ptr out_t, int acc) {
+    fx_dropout_bwd_colsum(dt, CP(dout), P(dx), F(part), rows, cols, splits, p, key, S(st),
+                          reinterpret_cast<int*>(cnt), F(out_f32), P(out_t), acc);
+  }, py::arg("dt"), py::arg("dout"), py::arg("dx"), py::arg("part"), py::arg("rows"),
+     py::arg("cols"), py::arg("splits"), py::arg("p"), py::arg("key"), py::arg("st"),
+     py::arg("cnt") = 0, py::arg("out_f32") = 0, py::arg("out_t") = 0, py::arg("acc") = 0);
   m.def("dropout_fwd", [](int dt, ptr x, ptr y, long n, float p, uint64_t key, ptr st) {
     fx_dropout_fwd(dt, CP(x), P(y), n, p, key, S(st));
   });
@@ -276,6 +300,24 @@ PYBIND11_MODULE(_kernels, m) {
                           ldy, P(kc), P(vc), reinterpret_cast<const long*>(pos), heads, head_dim,
                           maxlen, CP(ln_w), CP(ln_b), ln_eps, S(st));
   });
+  // one persistent launch per decoder layer (decode_layer.hip); args as a dict
+  // of pointers / ints / floats to keep the call readable
+  m.def("decode_layer", [](py::dict d) {
+    auto I = [&](const char* k) { return d[k].cast<long>(); };
+    auto Fl = [&](const char* k) { return d[k].cast<float>(); };
+    auto Pt = [&](const char* k) { return reinterpret_cast<void*>(d[k].cast<ptr>()); };
+    return fx_decode_layer(
+        (int)I("dt"), (int)I("M"), (int)I("h"), (int)I("ffn"), (int)I("heads"), (int)I("hd"),
+        (int)I("maxlen"), (int)I("nsplit"), Pt("x"), Pt("xout"), Pt("q"),
+        reinterpret_cast<float*>(Pt("apart")), Pt("x2"), Pt("f"), Pt("ln1w"), Pt("ln1b"),
+        Pt("wqkv"), Pt("bqkv"), Pt("wo"), Pt("bo"), Pt("ln2w"), Pt("ln2b"), Pt("w1"), Pt("b1"),
+        Pt("w2"), Pt("b2"), Pt("kc"), Pt("vc"), reinterpret_cast<const long*>(Pt("pos")),
+        reinterpret_cast<const int*>(Pt("lens")), Fl("eps1"), Fl("eps2"), Fl("scale"),
+        reinterpret_cast<unsigned*>(Pt("bar")), (unsigned)I("bar_base"),
+        reinterpret_cast<int*>(Pt("err")), S(d["st"].cast<ptr>()));
+  });
+  m.def("decode_layer_grid", &fx_decode_layer_grid);
+  m.def("decode_layer_barriers", &fx_decode_layer_barriers);
   // graph mode: device-resident dropout salt / AdamW learning rate (0 = off)
   m.def("set_dropout_salt", [](ptr p) { fx_set_dropout_salt(CP(p)); });
   m.def("set_adamw_lr_ptr", [](ptr p) { fx_set_adamw_lr_ptr(CP(p)); });

@@ -283,6 +283,99 @@ __global__ __launch_bounds__(256) void ln_bwd_row_generic(
 }
 
 // ---------------------------------------------------------------------------
+// Fused finalize of the column-sum partials: the LAST workgroup of each
+// 128-column tile to finish (ticket per tile) sums the tile's `splits`
+// partial rows in a fixed order (deterministic whoever arrives last) and
+// writes the outputs -- instead of a separate finalize launch per reduction
+// (~5-6 us each, 190-260 per training step).  Hand-off (cdna_hip_programming.md
+// §6 G16, sc1 form): the partials are stored write-through (sc1), every
+// storing wave drains them, workgroup barrier, one lane draws the ticket with
+// a relaxed agent-scope add; the last one reads the partials with sc1 loads
+// (16-byte buffer loads, aux = sc1).
+// No agent release fence: that is a write-back of the whole XCD L2, and these
+// kernels have just dirtied it with their dx output (measured: the
+// fence form made the four column kernels 2.5-4x slower than kernel + separate
+// finalize).  The last arriver resets the ticket (tickets are per stream,
+// zeroed once at allocation).  Each tile's ticket has a 128-byte line of its
+// own: device-scope atomics on one line serialise (~13 ns each), and with the
+// tickets packed the ~1024 arrivals of a short launch queued for ~13 us.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) float gf32;
+typedef __attribute__((address_space(1))) int gi32;
+
+__device__ __forceinline__ void st_part(float* p, float v) {   // sc1 store
+  __hip_atomic_store((gf32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct ColFin {
+  int* cnt;               // [col tiles x 32] tickets, one per 128-B line; nullptr = caller finalizes
+  float* f32[2];          // fp32 outputs (e.g. main_grad) for partial 0 / 1
+  uint16_t* t16[2];       // 16-bit outputs
+  int acc[2];             // accumulate into f32 (1) or overwrite (0)
+};
+
+template <typename T>
+__device__ __forceinline__ void colsum_tail(const float* __restrict__ p0,
+                                            const float* __restrict__ p1, int cols, int np,
+                                            const ColFin& f) {
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add((gi32*)(f.cnt + 32 * blockIdx.x), 1, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    last = t == (int)gridDim.y - 1;
+    if (last)
+      __hip_atomic_store((gi32*)(f.cnt + 32 * blockIdx.x), 0, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the loads below the ticket
+  // The reducer reads splits x 128 fp32 per array.  sc1-stored partials are not
+  // in any L2, so every read pays the fabric latency: issue them ALL at once
+  // -- 16-byte sc1 buffer loads, 32 lanes per split row (4 columns each), 8
+  // split rows per pass, 16 passes in flight per thread (128 split rows per
+  // round trip; out-of-range rows read 0 through the buffer range check) --
+  // then combine the 8 row phases through LDS in a fixed order.
+  __shared__ float tr[8][132];
+  const int q = threadIdx.x & 31, sr = threadIdx.x >> 5;
+  const int c0 = blockIdx.x * 128 + q * 4;
+  const int splits = gridDim.y;
+  for (int which = 0; which < np; ++which) {
+    const float* p = which ? p1 : p0;
+    floatx4 s = {0.f, 0.f, 0.f, 0.f};
+    if (c0 < cols) {
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0,
+                                                        splits * cols * 4, 0x00020000);
+      for (int k0 = sr; k0 < splits; k0 += 128) {
+        floatx4 v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int k = k0 + 8 * u;
+          const uint32_t off = k < splits ? (uint32_t)(k * cols + c0) * 4u : 0x80000000u;
+          v[u] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s += v[u];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tr[sr][q * 4 + j] = s[j];
+    __syncthreads();
+    const int c = threadIdx.x, gc = blockIdx.x * 128 + c;
+    if (c < 128 && gc < cols) {
+      float sum = 0.f;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) sum += tr[t][c];
+      if (f.f32[which]) f.f32[which][gc] = f.acc[which] ? f.f32[which][gc] + sum : sum;
+      if (f.t16[which]) f.t16[which][gc] = Elt<T>::from_f(sum);
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Column-tile partial sums.  Block = 256 threads = 16 column groups (8 cols
 // each -> 128 columns) x 16 row lanes.  Grid = (col tiles, splits).
 // MODE 0: LN  -> p0 += dy*xhat, p1 += dy            (a = dy, b = s)
@@ -292,7 +385,8 @@ template <typename T, int MODE>
 __global__ __launch_bounds__(256) void coltile_partial_kernel(
     const uint16_t* __restrict__ a, const uint16_t* __restrict__ b,
     const float* __restrict__ mean, const float* __restrict__ rstd,
-    float* __restrict__ p0, float* __restrict__ p1, int rows, int cols, int rows_per_split) {
+    float* __restrict__ p0, float* __restrict__ p1, int rows, int cols, int rows_per_split,
+    ColFin fin) {
   __shared__ float red[2][16][129];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int col = blockIdx.x * 128 + tx * 8;
@@ -329,12 +423,14 @@ __global__ __launch_bounds__(256) void coltile_partial_kernel(
   __syncthreads();
   // 256 threads reduce 128 columns x 2 arrays over 16 rows
   const int which = threadIdx.x >> 7, c = threadIdx.x & 127;
-  if (MODE == 1 && which == 1) return;
-  float s = 0.f;
+  if (MODE == 0 || which == 0) {
+    float s = 0.f;
 #pragma unroll
-  for (int t = 0; t < 16; ++t) s += red[which][t][c];
-  const int gc = blockIdx.x * 128 + c;
-  if (gc < cols) (which == 0 ? p0 : p1)[(size_t)blockIdx.y * cols + gc] = s;
+    for (int t = 0; t < 16; ++t) s += red[which][t][c];
+    const int gc = blockIdx.x * 128 + c;
+    if (gc < cols) st_part((which == 0 ? p0 : p1) + (size_t)blockIdx.y * cols + gc, s);
+  }
+  if (fin.cnt) colsum_tail<T>(p0, p1, cols, MODE == 0 ? 2 : 1, fin);
 }
 
 // Sum partials over splits; write fp32 and/or 16-bit outputs.
@@ -387,7 +483,7 @@ template <typename T, bool ERF>
 __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
     const uint16_t* __restrict__ bias, uint16_t* __restrict__ dx, float* __restrict__ part,
-    int rows, int cols, int rows_per_split) {
+    int rows, int cols, int rows_per_split, ColFin fin) {
   __shared__ float red[16][129];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int col = blockIdx.x * 128 + tx * 8;
@@ -427,8 +523,9 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(
 #pragma unroll
     for (int t = 0; t < 16; ++t) s += red[t][threadIdx.x];
     const int gc = blockIdx.x * 128 + threadIdx.x;
-    if (part && gc < cols) part[(size_t)blockIdx.y * cols + gc] = s;
+    if (part && gc < cols) st_part(part + (size_t)blockIdx.y * cols + gc, s);
   }
+  if (fin.cnt) colsum_tail<T>(part, nullptr, cols, 1, fin);
 }
 
 // ---------------------------------------------------------------------------
@@ -467,7 +564,7 @@ __global__ __launch_bounds__(256) void bias_dropout_add_fwd_kernel(
 template <typename T>
 __global__ __launch_bounds__(256) void dropout_bwd_colsum_kernel(
     const uint16_t* __restrict__ dout, uint16_t* __restrict__ dx, float* __restrict__ part,
-    int rows, int cols, int rows_per_split, DropCfg drop_) {
+    int rows, int cols, int rows_per_split, DropCfg drop_, ColFin fin) {
   const DropCfg drop = resolve_drop(drop_);
   __shared__ float red[16][129];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
@@ -501,8 +598,9 @@ __global__ __launch_bounds__(256) void dropout_bwd_colsum_kernel(
 #pragma unroll
     for (int t = 0; t < 16; ++t) s += red[t][threadIdx.x];
     const int gc = blockIdx.x * 128 + threadIdx.x;
-    if (part && gc < cols) part[(size_t)blockIdx.y * cols + gc] = s;
+    if (part && gc < cols) st_part(part + (size_t)blockIdx.y * cols + gc, s);
   }
+  if (fin.cnt) colsum_tail<T>(part, nullptr, cols, 1, fin);
 }
 
 // Plain dropout (embedding / generic): y = dropout(x)
@@ -540,8 +638,14 @@ inline int grid_for(long n8) {
 }
 
 inline int splits_for(int rows, int cols) {
+  // ~1024 workgroups per column reduction (FLEETX_COLSUM_BLOCKS overrides)
+  static const int blocks = [] {
+    const char* e = getenv("FLEETX_COLSUM_BLOCKS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 1024;
+  }();
   int tiles = (cols + 127) / 128;
-  int s = 1024 / (tiles > 0 ? tiles : 1);
+  int s = blocks / (tiles > 0 ? tiles : 1);
   if (s < 1) s = 1;
   int max_s = (rows + 15) / 16;
   if (s > max_s) s = max_s;
@@ -563,6 +667,17 @@ inline int splits_for(int rows, int cols) {
     using T = f16;                       \
     __VA_ARGS__;                         \
   }
+
+// Fused finalize arguments of the column-sum producers (cnt == nullptr: the
+// caller runs coltile_finalize itself).
+static ColFin make_fin(int* cnt, float* f0, void* t0, int acc0, float* f1, void* t1, int acc1) {
+  ColFin f;
+  f.cnt = cnt;
+  f.f32[0] = f0; f.f32[1] = f1;
+  f.t16[0] = (uint16_t*)t0; f.t16[1] = (uint16_t*)t1;
+  f.acc[0] = acc0; f.acc[1] = acc1;
+  return f;
+}
 
 extern "C" int fx_coltile_splits(int rows, int cols) { return splits_for(rows, cols); }
 
@@ -634,17 +749,19 @@ extern "C" void fx_ln_bwd_row(int dtype, const void* dy, const void* s, const fl
 // dgamma/dbeta partials (mode 0) or plain column sum partials (mode 1).
 extern "C" void fx_coltile_partial(int dtype, int mode, const void* a, const void* b,
                                    const float* mean, const float* rstd, float* p0, float* p1,
-                                   int rows, int cols, int splits, hipStream_t st) {
+                                   int rows, int cols, int splits, hipStream_t st, int* cnt,
+                                   float* f0, void* t0, int acc0, float* f1, void* t1, int acc1) {
+  const ColFin fin = make_fin(cnt, f0, t0, acc0, f1, t1, acc1);
   int rps = (rows + splits - 1) / splits;
   dim3 grid((cols + 127) / 128, splits), block(256);
   auto A = (const uint16_t*)a;
   auto B = (const uint16_t*)b;
   if (mode == 0) {
     FX_DISPATCH_T(dtype, coltile_partial_kernel<T, 0><<<grid, block, 0, st>>>(
-                             A, B, mean, rstd, p0, p1, rows, cols, rps));
+                             A, B, mean, rstd, p0, p1, rows, cols, rps, fin));
   } else {
     FX_DISPATCH_T(dtype, coltile_partial_kernel<T, 1><<<grid, block, 0, st>>>(
-                             A, B, mean, rstd, p0, p1, rows, cols, rps));
+                             A, B, mean, rstd, p0, p1, rows, cols, rps, fin));
   }
 }
 
@@ -669,17 +786,19 @@ extern "C" void fx_bias_gelu_fwd(int dtype, int erf, const void* x, const void* 
 
 extern "C" void fx_bias_gelu_bwd(int dtype, int erf, const void* dy, const void* x,
                                  const void* bias, void* dx, float* part, int rows, int cols,
-                                 int splits, hipStream_t st) {
+                                 int splits, hipStream_t st, int* cnt, float* out_f32,
+                                 void* out_t, int acc) {
+  const ColFin fin = make_fin(cnt, out_f32, out_t, acc, nullptr, nullptr, 0);
   int rps = (rows + splits - 1) / splits;
   dim3 grid((cols + 127) / 128, splits), block(256);
   if (erf) {
     FX_DISPATCH_T(dtype, bias_gelu_bwd_kernel<T, true><<<grid, block, 0, st>>>(
                              (const uint16_t*)dy, (const uint16_t*)x, (const uint16_t*)bias,
-                             (uint16_t*)dx, part, rows, cols, rps));
+                             (uint16_t*)dx, part, rows, cols, rps, fin));
   } else {
     FX_DISPATCH_T(dtype, bias_gelu_bwd_kernel<T, false><<<grid, block, 0, st>>>(
                              (const uint16_t*)dy, (const uint16_t*)x, (const uint16_t*)bias,
-                             (uint16_t*)dx, part, rows, cols, rps));
+                             (uint16_t*)dx, part, rows, cols, rps, fin));
   }
 }
 
@@ -695,12 +814,14 @@ extern "C" void fx_bias_dropout_add_fwd(int dtype, const void* x, const void* bi
 
 extern "C" void fx_dropout_bwd_colsum(int dtype, const void* dout, void* dx, float* part,
                                       int rows, int cols, int splits, float p, uint64_t key,
-                                      hipStream_t st) {
+                                      hipStream_t st, int* cnt, float* out_f32, void* out_t,
+                                      int acc) {
+  const ColFin fin = make_fin(cnt, out_f32, out_t, acc, nullptr, nullptr, 0);
   DropCfg d = make_drop(p, key);
   int rps = (rows + splits - 1) / splits;
   dim3 grid((cols + 127) / 128, splits), block(256);
   FX_DISPATCH_T(dtype, dropout_bwd_colsum_kernel<T><<<grid, block, 0, st>>>(
-                           (const uint16_t*)dout, (uint16_t*)dx, part, rows, cols, rps, d));
+                           (const uint16_t*)dout, (uint16_t*)dx, part, rows, cols, rps, d, fin));
 }
 
 extern "C" void fx_dropout_fwd(int dtype, const void* x, void* y, long n, float p, uint64_t key,

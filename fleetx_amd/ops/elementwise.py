@@ -58,12 +58,14 @@ class _BiasGelu(torch.autograd.Function):
             dx = torch.empty_like(x)
             dc = _lib.dt_code(x.dtype)
             st = _lib.stream()
-            k.bias_gelu_bwd(dc, int(ctx.erf), dy.data_ptr(), x.data_ptr(), _lib.ptr(bias),
-                            dx.data_ptr(), part.data_ptr(), rows, cols, splits, st)
             db = None
+            fin = {}
             if ctx.has_bias:
                 db = torch.empty(cols, device=x.device, dtype=bias.dtype)
-                k.coltile_finalize(dc, part.data_ptr(), splits, cols, 0, db.data_ptr(), 0, st)
+                from .norm import colsum_tickets
+                fin = {"cnt": colsum_tickets(x.device, cols), "out_t": db.data_ptr()}
+            k.bias_gelu_bwd(dc, int(ctx.erf), dy.data_ptr(), x.data_ptr(), _lib.ptr(bias),
+                            dx.data_ptr(), part.data_ptr(), rows, cols, splits, st, **fin)
         else:
             t = x.float() + (bias.float() if bias is not None else 0.0)
             dx = (dy.float() * _gelu_grad_ref(t, ctx.erf)).to(x.dtype)
@@ -100,12 +102,14 @@ def gelu_grad(dy, h, erf=False, colsum=None):
         part = torch.empty(splits, cols, device=h.device, dtype=torch.float32)
         dx = torch.empty_like(h)
         dc = _lib.dt_code(h.dtype)
-        k.bias_gelu_bwd(dc, int(erf), dy.data_ptr(), h.data_ptr(), 0,
-                        dx.data_ptr(), part.data_ptr(), rows, cols, splits, _lib.stream())
+        fin = {}
         if colsum is not None:
             dst, acc = colsum
-            k.coltile_finalize(dc, part.data_ptr(), splits, cols, dst.data_ptr(), 0, int(acc),
-                               _lib.stream())
+            from .norm import colsum_tickets
+            fin = {"cnt": colsum_tickets(h.device, cols), "out_f32": dst.data_ptr(),
+                   "acc": int(acc)}
+        k.bias_gelu_bwd(dc, int(erf), dy.data_ptr(), h.data_ptr(), 0,
+                        dx.data_ptr(), part.data_ptr(), rows, cols, splits, _lib.stream(), **fin)
         return dx
     dx = (dy.float() * _gelu_grad_ref(h.float(), erf)).to(h.dtype)
     if colsum is not None:
@@ -153,18 +157,23 @@ class _BiasDropoutAdd(torch.autograd.Function):
             if ctx.has_bias:
                 splits = k.coltile_splits(rows, cols)
                 part = torch.empty(splits, cols, device=dout.device, dtype=torch.float32)
-                k.dropout_bwd_colsum(dc, dout.data_ptr(), dx.data_ptr() if ctx.p > 0 else 0,
-                                     part.data_ptr(), rows, cols, splits, float(ctx.p), ctx.key, st)
+                from .norm import colsum_tickets
                 bias = ctx.bias
-                if bias is not None and getattr(bias, "_fx_fused_wgrad", False) \
-                        and hasattr(bias, "main_grad"):
-                    # fp32 bias gradient straight into main_grad
-                    from .norm import _into_main_grad
-                    _into_main_grad(bias, lambda mg, acc: k.coltile_finalize(
-                        dc, part.data_ptr(), splits, cols, mg.data_ptr(), 0, int(acc), st))
+                fused = bias is not None and getattr(bias, "_fx_fused_wgrad", False) \
+                    and hasattr(bias, "main_grad")
+                if fused:  # fp32 bias gradient straight into main_grad
+                    fin = {"out_f32": bias.main_grad.data_ptr(),
+                           "acc": int(not getattr(bias, "_fx_fresh", False))}
                 else:
                     db = torch.empty(cols, device=dout.device, dtype=dout.dtype)
-                    k.coltile_finalize(dc, part.data_ptr(), splits, cols, 0, db.data_ptr(), 0, st)
+                    fin = {"out_t": db.data_ptr()}
+                k.dropout_bwd_colsum(dc, dout.data_ptr(), dx.data_ptr() if ctx.p > 0 else 0,
+                                     part.data_ptr(), rows, cols, splits, float(ctx.p), ctx.key, st,
+                                     cnt=colsum_tickets(dout.device, cols), **fin)
+                if fused:
+                    from ..parallel.linear import grad_part_done
+                    bias._fx_fresh = False
+                    grad_part_done(bias)
             elif ctx.p > 0:
                 k.dropout_fwd(dc, dout.data_ptr(), dx.data_ptr(), dout.numel(), float(ctx.p),
                               ctx.key, st)

@@ -12,6 +12,24 @@ from . import _lib
 from ..parallel import rng as _rng
 
 
+_TICKETS = {}
+
+
+def colsum_tickets(device, cols):
+    """Ticket array of the fused column-sum finalize (the last workgroup of a
+    128-column tile sums the splits; csrc/kernels/norm_eltwise.hip
+    ``colsum_tail``), one per stream: zeroed once, each launch's last
+    workgroup resets its tiles' tickets.  One ticket per 128-byte line (32
+    int32 per 128-column tile): arrivals on one line serialise."""
+    st = torch.cuda.current_stream(device).cuda_stream
+    need = 32 * ((cols + 127) // 128)
+    t = _TICKETS.get(st)
+    if t is None or t.numel() < need:
+        t = torch.zeros(max(4096, need), dtype=torch.int32, device=device)
+        _TICKETS[st] = t
+    return t.data_ptr()
+
+
 def _col_reduce_ln(dy, s, mean, rstd, cols, dtype):
     k = _lib.kernels()
     rows = dy.numel() // cols
@@ -20,12 +38,11 @@ def _col_reduce_ln(dy, s, mean, rstd, cols, dtype):
     p1 = torch.empty_like(p0)
     st = _lib.stream()
     dc = _lib.dt_code(dtype)
-    k.coltile_partial(dc, 0, dy.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-                      p0.data_ptr(), p1.data_ptr(), rows, cols, splits, st)
     dg = torch.empty(cols, device=dy.device, dtype=dtype)
     db = torch.empty(cols, device=dy.device, dtype=dtype)
-    k.coltile_finalize(dc, p0.data_ptr(), splits, cols, 0, dg.data_ptr(), 0, st)
-    k.coltile_finalize(dc, p1.data_ptr(), splits, cols, 0, db.data_ptr(), 0, st)
+    k.coltile_partial(dc, 0, dy.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                      p0.data_ptr(), p1.data_ptr(), rows, cols, splits, st,
+                      cnt=colsum_tickets(dy.device, cols), t0=dg.data_ptr(), t1=db.data_ptr())
     return dg, db
 
 
@@ -52,11 +69,15 @@ def _col_reduce_ln_main_grad(dy, s, mean, rstd, cols, dtype, weight, lnbias):
     p1 = torch.empty_like(p0)
     st = _lib.stream()
     dc = _lib.dt_code(dtype)
+    acc = [int(not getattr(prm, "_fx_fresh", False)) for prm in (weight, lnbias)]
     k.coltile_partial(dc, 0, dy.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-                      p0.data_ptr(), p1.data_ptr(), rows, cols, splits, st)
-    for prm, part in ((weight, p0), (lnbias, p1)):
-        _into_main_grad(prm, lambda mg, acc, part=part: k.coltile_finalize(
-            dc, part.data_ptr(), splits, cols, mg.data_ptr(), 0, int(acc), st))
+                      p0.data_ptr(), p1.data_ptr(), rows, cols, splits, st,
+                      cnt=colsum_tickets(dy.device, cols), f0=weight.main_grad.data_ptr(),
+                      acc0=acc[0], f1=lnbias.main_grad.data_ptr(), acc1=acc[1])
+    from ..parallel.linear import grad_part_done
+    for prm in (weight, lnbias):
+        prm._fx_fresh = False
+        grad_part_done(prm)
 
 
 def col_sum(x, cols):
@@ -69,9 +90,9 @@ def col_sum(x, cols):
     p0 = torch.empty(splits, cols, device=x.device, dtype=torch.float32)
     st = _lib.stream()
     dc = _lib.dt_code(x.dtype)
-    k.coltile_partial(dc, 1, x.data_ptr(), 0, 0, 0, p0.data_ptr(), 0, rows, cols, splits, st)
     out = torch.empty(cols, device=x.device, dtype=x.dtype)
-    k.coltile_finalize(dc, p0.data_ptr(), splits, cols, 0, out.data_ptr(), 0, st)
+    k.coltile_partial(dc, 1, x.data_ptr(), 0, 0, 0, p0.data_ptr(), 0, rows, cols, splits, st,
+                      cnt=colsum_tickets(x.device, cols), t0=out.data_ptr())
     return out
 
 
@@ -95,8 +116,9 @@ def col_sum_f32(x, dst, accumulate=False):
     p0 = torch.empty(splits, cols, device=x.device, dtype=torch.float32)
     st = _lib.stream()
     dc = _lib.dt_code(x.dtype)
-    k.coltile_partial(dc, 1, x.data_ptr(), 0, 0, 0, p0.data_ptr(), 0, rows, cols, splits, st)
-    k.coltile_finalize(dc, p0.data_ptr(), splits, cols, dst.data_ptr(), 0, int(accumulate), st)
+    k.coltile_partial(dc, 1, x.data_ptr(), 0, 0, 0, p0.data_ptr(), 0, rows, cols, splits, st,
+                      cnt=colsum_tickets(x.device, cols), f0=dst.data_ptr(),
+                      acc0=int(accumulate))
     return dst
 
 

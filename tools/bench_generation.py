@@ -51,7 +51,10 @@ def main():
             torch.cuda.synchronize()
             t = time.perf_counter() - t0
             ms = 1e3 * (t - t_pre) / max(1, ids.shape[1] - 1)
+            persistent = fused and B <= 4 and \
+                os.environ.get("FLEETX_DECODE_PERSISTENT", "0") == "1"
             print(json.dumps({"model": args.model, "batch": B, "fused_decode": fused,
+                              "persistent_layers": persistent,
                               "ms_per_token": round(ms, 3),
                               "tokens_per_s": round(B * 1e3 / ms, 1),
                               "weight_TB_s": round(nbytes / (ms * 1e-3) / 1e12, 2)}), flush=True)
