@@ -18,6 +18,10 @@ void fx_add_ln_fwd(int, const void*, const void*, const void*, const void*, cons
                    void*, float*, float*, int, int, float, float, uint64_t, hipStream_t);
 void fx_ln_bwd_row(int, const void*, const void*, const float*, const float*, const void*,
                    const void*, void*, void*, int, int, float, uint64_t, hipStream_t);
+int fx_ln_bwd_cols_blocks(int, int);
+int fx_ln_bwd_cols(int, const void*, const void*, const float*, const float*, const void*,
+                   const void*, void*, void*, int, int, float, uint64_t, float*, int, float*, void*,
+                   int, float*, void*, int, float*, void*, int, hipStream_t);
 void fx_coltile_partial(int, int, const void*, const void*, const float*, const float*, float*,
                         float*, int, int, int, hipStream_t, int*, float*, void*, int, float*,
                         void*, int);
@@ -125,6 +129,22 @@ PYBIND11_MODULE(_kernels, m) {
     fx_ln_bwd_row(dt, CP(dy), CP(s), F(mean), F(rstd), CP(g), CP(ds_in), P(ds_out), P(dx_out),
                   rows, h, p, key, S(st));
   });
+  // LayerNorm backward with dgamma / dbeta (/ dbias of the fused residual's
+  // linear) column sums in the same pass; returns -1 if h is not covered
+  m.def("ln_bwd_cols_blocks", &fx_ln_bwd_cols_blocks);
+  m.def("ln_bwd_cols", [](int dt, ptr dy, ptr s, ptr mean, ptr rstd, ptr g, ptr ds_in, ptr ds_out,
+                          ptr dx_out, int rows, int h, float p, uint64_t key, ptr part,
+                          int with_dbias, ptr fg, ptr tg, int accg, ptr fb, ptr tb, int accb,
+                          ptr fx, ptr tx, int accx, ptr st) {
+    return fx_ln_bwd_cols(dt, CP(dy), CP(s), F(mean), F(rstd), CP(g), CP(ds_in), P(ds_out),
+                          P(dx_out), rows, h, p, key, F(part), with_dbias, F(fg), P(tg), accg,
+                          F(fb), P(tb), accb, F(fx), P(tx), accx, S(st));
+  }, py::arg("dt"), py::arg("dy"), py::arg("s"), py::arg("mean"), py::arg("rstd"), py::arg("g"),
+     py::arg("ds_in"), py::arg("ds_out"), py::arg("dx_out"), py::arg("rows"), py::arg("h"),
+     py::arg("p"), py::arg("key"), py::arg("part"), py::arg("with_dbias"), py::arg("fg") = 0,
+     py::arg("tg") = 0, py::arg("accg") = 0, py::arg("fb") = 0, py::arg("tb") = 0,
+     py::arg("accb") = 0, py::arg("fx") = 0, py::arg("tx") = 0, py::arg("accx") = 0,
+     py::arg("st") = 0);
   // column-sum producers: cnt != 0 fuses the finalize (last workgroup of a
   // column tile sums the splits into f*/t* outputs); cnt == 0: the caller
   // runs coltile_finalize

@@ -47,7 +47,9 @@ __device__ __forceinline__ float drop_apply(float v, uint64_t idx, const DropCfg
 // Any of residual/bias may be null; dropout optional.  If s_out is null the
 // sum is not stored (plain LN when residual & bias are null and no dropout).
 // ---------------------------------------------------------------------------
-template <typename T, int VPT>
+// MASK: h is not a multiple of 512 (ViT-g 1408, ViT-B 768): the last vector
+// of some lanes lies past the row end and is neither loaded nor counted.
+template <typename T, int VPT, bool MASK = false>
 __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ bias,
     const uint16_t* __restrict__ residual, const uint16_t* __restrict__ gamma,
@@ -64,6 +66,11 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int c = (i * 64 + lane) * 8;
+    if (MASK && c >= h) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+      continue;
+    }
     load8<T>(x + base + c, v[i]);
     if (bias) {
       float b[8];
@@ -94,16 +101,19 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
   const float mean = wave_sum(sum) / h;
   float var = 0.f;
 #pragma unroll
-  for (int i = 0; i < VPT; ++i)
+  for (int i = 0; i < VPT; ++i) {
+    if (MASK && (i * 64 + lane) * 8 >= h) continue;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float d = v[i][j] - mean;
       var += d * d;
     }
+  }
   const float rstd = rsqrtf(wave_sum(var) / h + eps);
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int c = (i * 64 + lane) * 8;
+    if (MASK && c >= h) continue;
     float g[8], b[8], o[8];
     load8<T>(gamma + c, g);
     load8<T>(beta + c, b);
@@ -179,7 +189,7 @@ __global__ __launch_bounds__(256) void add_ln_fwd_generic(
 // Row backward:  ds = ds_in + LN'(dy);  dx = dropout'(ds)
 //   s: the LN input (as stored), dx_out may alias ds_out when no dropout.
 // ---------------------------------------------------------------------------
-template <typename T, int VPT>
+template <typename T, int VPT, bool MASK = false>
 __global__ __launch_bounds__(256) void ln_bwd_row_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ s,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
@@ -197,6 +207,11 @@ __global__ __launch_bounds__(256) void ln_bwd_row_kernel(
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int c = (i * 64 + lane) * 8;
+    if (MASK && c >= h) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xh[i][j] = gdy[i][j] = 0.f;
+      continue;
+    }
     float a[8], g[8], d[8];
     load8<T>(s + base + c, a);
     load8<T>(gamma + c, g);
@@ -213,6 +228,7 @@ __global__ __launch_bounds__(256) void ln_bwd_row_kernel(
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int c = (i * 64 + lane) * 8;
+    if (MASK && c >= h) continue;
     float o[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = rstd * (gdy[i][j] - m1 - xh[i][j] * m2);
@@ -280,6 +296,188 @@ __global__ __launch_bounds__(256) void ln_bwd_row_generic(
       store8<T>(dx_out + base + c, o);
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Row backward + its column sums in one pass (h <= 1536):
+//   ds = ds_in + LN'(dy),  dx = dropout'(ds)          (as ln_bwd_row_kernel)
+//   dgamma = sum dy * xhat,  dbeta = sum dy,  dbias = sum dx (optional: the
+//   bias of the linear that feeds the fused residual add)
+// instead of the row kernel + two column-tile passes that re-read dy and s
+// (reference K07's LayerNorm backward + the bias gradient of K09).  Each wave
+// owns a contiguous run of rows, keeps its columns' sums in registers and
+// loads the next row while it reduces the current one; gamma is read once
+// per wave.  The 4 waves' sums meet in LDS in a fixed order and the block
+// writes one partial row per array ([3][G][h] fp32); ln_cols_finalize_kernel
+// adds the G rows in a fixed order -- bitwise reproducible.
+// ---------------------------------------------------------------------------
+template <typename T, int VPT, bool MASK, bool DB>
+__global__ __launch_bounds__(256) void ln_bwd_cols_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ s,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    const uint16_t* __restrict__ gamma, const uint16_t* __restrict__ ds_in,
+    uint16_t* __restrict__ ds_out, uint16_t* __restrict__ dx_out, int rows, int h,
+    int rows_per_wave, float* __restrict__ part, DropCfg drop_) {
+  __shared__ float red[4 * 512 * VPT];
+  const DropCfg drop = resolve_drop(drop_);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r0 = min(rows, (blockIdx.x * 4 + w) * rows_per_wave);
+  const int r1 = min(rows, r0 + rows_per_wave);
+  float g[VPT][8], ag[VPT][8], ab[VPT][8], ax[DB ? VPT : 1][8];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = (i * 64 + lane) * 8;
+    if (!MASK || c < h) {
+      load8<T>(gamma + c, g[i]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[i][j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ag[i][j] = ab[i][j] = 0.f;
+      if (DB) ax[i][j] = 0.f;
+    }
+  }
+  // next-row prefetch only where the registers allow two waves per SIMD
+  constexpr bool PF = VPT <= 2;
+  uint4 na[VPT], nd[VPT], nr[VPT];
+  auto fetch = [&](int r) {
+    const size_t base = (size_t)r * h;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      if (MASK && c >= h) continue;
+      na[i] = *reinterpret_cast<const uint4*>(s + base + c);
+      nd[i] = *reinterpret_cast<const uint4*>(dy + base + c);
+      if (ds_in) nr[i] = *reinterpret_cast<const uint4*>(ds_in + base + c);
+    }
+  };
+  if (PF && r0 < r1) fetch(r0);
+  for (int r = r0; r < r1; ++r) {
+    if (!PF) fetch(r);
+    uint4 ca[VPT], cd[VPT], cr[VPT];
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      ca[i] = na[i];
+      cd[i] = nd[i];
+      cr[i] = nr[i];
+    }
+    if (PF && r + 1 < r1) fetch(r + 1);
+    const size_t base = (size_t)r * h;
+    const float mean = mean_in[r], rstd = rstd_in[r];
+    float xh[VPT][8], dd[VPT][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      if (MASK && c >= h) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xh[i][j] = dd[i][j] = 0.f;
+        continue;
+      }
+      float a[8];
+      unpack8<T>(ca[i], a);
+      unpack8<T>(cd[i], dd[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xh[i][j] = (a[j] - mean) * rstd;
+        const float gd = dd[i][j] * g[i][j];
+        s1 += gd;
+        s2 += gd * xh[i][j];
+      }
+    }
+    const float m1 = wave_sum(s1) / h, m2 = wave_sum(s2) / h;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      if (MASK && c >= h) continue;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = rstd * (dd[i][j] * g[i][j] - m1 - xh[i][j] * m2);
+        ag[i][j] += dd[i][j] * xh[i][j];
+        ab[i][j] += dd[i][j];
+      }
+      if (ds_in) {
+        float rr[8];
+        unpack8<T>(cr[i], rr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += rr[j];
+      }
+      store8<T>(ds_out + base + c, o);
+      if (drop.enabled) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = drop_apply(o[j], base + c + j, drop);
+        store8<T>(dx_out + base + c, o);
+      } else if (dx_out != ds_out) {
+        store8<T>(dx_out + base + c, o);
+      }
+      if (DB) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ax[i][j] += round_to<T>(o[j]);
+      }
+    }
+  }
+  // block partials: the 4 waves' column sums, added in wave order
+#pragma unroll
+  for (int arr = 0; arr < (DB ? 3 : 2); ++arr) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      if (MASK && c >= h) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        red[w * h + c + j] = arr == 0 ? ag[i][j] : arr == 1 ? ab[i][j] : ax[DB ? i : 0][j];
+    }
+    __syncthreads();
+    float* out = part + ((size_t)arr * gridDim.x + blockIdx.x) * h;
+    for (int c = threadIdx.x; c < h; c += 256)
+      out[c] = ((red[c] + red[h + c]) + red[2 * h + c]) + red[3 * h + c];
+  }
+}
+
+// Sum the G partial rows of each array ([narr][G][h]) per column in a fixed
+// order: 32 lanes x 4 columns per partial row, 8 row phases, 16 loads in
+// flight per thread; the 8 phases meet in LDS.  grid = (h / 128, narr).
+struct LnColsOut {
+  float* f32[3];
+  uint16_t* t16[3];
+  int acc[3];
+};
+template <typename T>
+__global__ __launch_bounds__(256) void ln_cols_finalize_kernel(const float* __restrict__ part,
+                                                               int G, int h, LnColsOut f) {
+  __shared__ float tr[8][132];
+  const int arr = blockIdx.y;
+  const float* p = part + (size_t)arr * G * h;
+  const int q = threadIdx.x & 31, sr = threadIdx.x >> 5;
+  const int c0 = blockIdx.x * 128 + q * 4;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (c0 < h) {
+    for (int k0 = sr; k0 < G; k0 += 128) {
+      floatx4 v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int k = k0 + 8 * u;
+        v[u] = k < G ? *reinterpret_cast<const floatx4*>(p + (size_t)k * h + c0)
+                     : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc += v[u];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) tr[sr][q * 4 + j] = acc[j];
+  __syncthreads();
+  const int c = threadIdx.x, gc = blockIdx.x * 128 + c;
+  if (c >= 128 || gc >= h) return;
+  float sum = 0.f;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) sum += tr[t][c];
+  if (f.f32[arr]) f.f32[arr][gc] = f.acc[arr] ? f.f32[arr][gc] + sum : sum;
+  if (f.t16[arr]) f.t16[arr][gc] = Elt<T>::from_f(sum);
 }
 
 // ---------------------------------------------------------------------------
@@ -707,6 +905,18 @@ extern "C" void fx_add_ln_fwd(int dtype, const void* x, const void* bias, const 
         FX_DISPATCH_T(dtype, add_ln_fwd_generic<T><<<grid, block, 0, st>>>(
                                  X, B, R, G, Be, S, Y, mean, rstd, rows, h, eps, d));
     }
+  } else if (h % 8 == 0 && h < 8 * 512) {
+    // row held in registers, last vector masked (ViT-g 1408: 2.75 vectors per lane)
+#define LNM_CASE(V)                                                                          \
+  case V:                                                                                    \
+    FX_DISPATCH_T(dtype, add_ln_fwd_kernel<T, V, true><<<grid, block, 0, st>>>(              \
+                             X, B, R, G, Be, S, Y, mean, rstd, rows, h, eps, d));            \
+    break;
+    switch ((h + 511) / 512) {
+      LNM_CASE(1) LNM_CASE(2) LNM_CASE(3) LNM_CASE(4) LNM_CASE(5) LNM_CASE(6) LNM_CASE(7)
+      LNM_CASE(8)
+    }
+#undef LNM_CASE
   } else {
     FX_DISPATCH_T(dtype, add_ln_fwd_generic<T><<<grid, block, 0, st>>>(
                              X, B, R, G, Be, S, Y, mean, rstd, rows, h, eps, d));
@@ -739,11 +949,79 @@ extern "C" void fx_ln_bwd_row(int dtype, const void* dy, const void* s, const fl
         FX_DISPATCH_T(dtype, ln_bwd_row_generic<T><<<grid, block, 0, st>>>(
                                  DY, S, mean, rstd, G, DI, DS, DX, rows, h, d));
     }
+  } else if (h % 8 == 0 && h < 8 * 512) {
+#define LNBM_CASE(V)                                                                      \
+  case V:                                                                                 \
+    FX_DISPATCH_T(dtype, ln_bwd_row_kernel<T, V, true><<<grid, block, 0, st>>>(           \
+                             DY, S, mean, rstd, G, DI, DS, DX, rows, h, d));              \
+    break;
+    switch ((h + 511) / 512) {
+      LNBM_CASE(1) LNBM_CASE(2) LNBM_CASE(3) LNBM_CASE(4) LNBM_CASE(5) LNBM_CASE(6)
+      LNBM_CASE(7) LNBM_CASE(8)
+    }
+#undef LNBM_CASE
   } else {
     FX_DISPATCH_T(dtype, ln_bwd_row_generic<T><<<grid, block, 0, st>>>(
                              DY, S, mean, rstd, G, DI, DS, DX, rows, h, d));
   }
 #undef LNB_CASE
+}
+
+// Fused LayerNorm backward (h % 8 == 0, h <= 1536): rows per wave and
+// partial rows G for a given row count (the caller sizes part = [3][G][h]).
+static int ln_cols_rows_per_wave(int rows) {
+  int rpw = (rows + 512 * 4 - 1) / (512 * 4);
+  return rpw < 2 ? 2 : rpw;
+}
+extern "C" int fx_ln_bwd_cols_blocks(int rows, int h) {
+  if (h % 8 || h > 1536 || rows <= 0) return 0;   // <= 3 vectors per lane: 2 waves / SIMD
+  const int rpw = ln_cols_rows_per_wave(rows);
+  return (rows + 4 * rpw - 1) / (4 * rpw);
+}
+
+// Returns 0 when launched, -1 when the shape is not covered.
+extern "C" int fx_ln_bwd_cols(int dtype, const void* dy, const void* s, const float* mean,
+                              const float* rstd, const void* gamma, const void* ds_in,
+                              void* ds_out, void* dx_out, int rows, int h, float p, uint64_t key,
+                              float* part, int with_dbias, float* fg, void* tg, int accg,
+                              float* fb, void* tb, int accb, float* fx, void* tx, int accx,
+                              hipStream_t st) {
+  const int G = fx_ln_bwd_cols_blocks(rows, h);
+  if (G == 0) return -1;
+  const int rpw = ln_cols_rows_per_wave(rows);
+  DropCfg d = make_drop(p, key);
+  auto DY = (const uint16_t*)dy;
+  auto S = (const uint16_t*)s;
+  auto GM = (const uint16_t*)gamma;
+  auto DI = (const uint16_t*)ds_in;
+  auto DS = (uint16_t*)ds_out;
+  auto DX = (uint16_t*)dx_out;
+  const int vpt = (h + 511) / 512;
+  const bool mask = h % 512 != 0;
+#define LNC_GO(V, M, DB)                                                                      \
+  FX_DISPATCH_T(dtype, ln_bwd_cols_kernel<T, V, M, DB><<<G, 256, 0, st>>>(                    \
+                           DY, S, mean, rstd, GM, DI, DS, DX, rows, h, rpw, part, d))
+#define LNC_V(V)                                                                              \
+  case V:                                                                                     \
+    if (mask) {                                                                               \
+      if (with_dbias) { LNC_GO(V, true, true); } else { LNC_GO(V, true, false); }             \
+    } else {                                                                                  \
+      if (with_dbias) { LNC_GO(V, false, true); } else { LNC_GO(V, false, false); }           \
+    }                                                                                         \
+    break;
+  switch (vpt) {
+    LNC_V(1) LNC_V(2) LNC_V(3)
+    default: return -1;
+  }
+#undef LNC_V
+#undef LNC_GO
+  LnColsOut f;
+  f.f32[0] = fg; f.f32[1] = fb; f.f32[2] = fx;
+  f.t16[0] = (uint16_t*)tg; f.t16[1] = (uint16_t*)tb; f.t16[2] = (uint16_t*)tx;
+  f.acc[0] = accg; f.acc[1] = accb; f.acc[2] = accx;
+  dim3 grid((h + 127) / 128, with_dbias ? 3 : 2);
+  FX_DISPATCH_T(dtype, ln_cols_finalize_kernel<T><<<grid, 256, 0, st>>>(part, G, h, f));
+  return 0;
 }
 
 // dgamma/dbeta partials (mode 0) or plain column sum partials (mode 1).

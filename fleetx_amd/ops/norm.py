@@ -6,6 +6,8 @@
 then LN2" in one HBM pass (reference K07 + K09,
 ``single_model.py:393-394,412``).
 """
+import os
+
 import torch
 
 from . import _lib
@@ -129,6 +131,51 @@ def _dropout_ref(x, p, key):
     return torch.where(m, x * (1.0 / (1.0 - p)), torch.zeros_like(x))
 
 
+# FLEETX_LN_BWD_FUSED=0 keeps the row kernel + column-tile passes (A/B)
+_LN_BWD_COLS = os.environ.get("FLEETX_LN_BWD_FUSED", "1") != "0"
+
+
+def _main_grad_target(p):
+    return _fused_param(p) and p.main_grad.dtype == torch.float32 and p.main_grad.is_contiguous()
+
+
+def _ln_bwd_cols(k, dc, dy, s, mean, rstd, weight, ctx, ds_in, ds, dx, rows, h):
+    """LayerNorm backward and its column sums (dgamma, dbeta and, with a fused
+    residual + bias, the bias gradient ``sum(dx)``) in one row pass plus one
+    small finalize launch (csrc/kernels/norm_eltwise.hip ``ln_bwd_cols_kernel``)
+    -- written into the fp32 ``main_grad`` where the parameter has one, else
+    returned as 16-bit gradients."""
+    G = k.ln_bwd_cols_blocks(rows, h)
+    with_db = bool(ctx.has_bias)
+    part = torch.empty(3 if with_db else 2, G, h, device=dy.device, dtype=torch.float32)
+    outs, grads, done = [], [], []
+    for prm, want in ((weight, True), (ctx.lnbias, True), (ctx.bias, with_db)):
+        if not want:
+            outs.append((0, 0, 0))
+            grads.append(None)
+        elif _main_grad_target(prm):
+            outs.append((prm.main_grad.data_ptr(), 0, int(not getattr(prm, "_fx_fresh", False))))
+            grads.append(None)
+            done.append(prm)
+        else:
+            g = torch.empty(h, device=dy.device, dtype=dy.dtype)
+            outs.append((0, g.data_ptr(), 0))
+            grads.append(g)
+    (fg, tg, ag), (fb, tb, ab), (fx, tx, ax) = outs
+    rc = k.ln_bwd_cols(dc, dy.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                       weight.data_ptr(), _lib.ptr(ds_in), ds.data_ptr(), dx.data_ptr(), rows, h,
+                       float(ctx.p), ctx.key, part.data_ptr(), int(with_db), fg, tg, ag, fb, tb,
+                       ab, fx, tx, ax, _lib.stream())
+    if rc != 0:
+        raise RuntimeError("ln_bwd_cols: shape rows=%d h=%d not covered" % (rows, h))
+    if done:
+        from ..parallel.linear import grad_part_done
+        for prm in done:
+            prm._fx_fresh = False
+            grad_part_done(prm)
+    return grads[0], grads[1], grads[2]
+
+
 class _AddLayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, bias, residual, weight, lnbias, eps, p, key, store_sum):
@@ -187,6 +234,11 @@ class _AddLayerNorm(torch.autograd.Function):
             dc = _lib.dt_code(dy.dtype)
             ds = torch.empty_like(dy)
             dx = torch.empty_like(dy) if ctx.p > 0 else ds
+            if _LN_BWD_COLS and k.ln_bwd_cols_blocks(rows, h) > 0:
+                dw, db, dbias = _ln_bwd_cols(k, dc, dy, s, mean, rstd, weight, ctx, ds_in, ds, dx,
+                                             rows, h)
+                dres = ds if ctx.has_res else None
+                return dx, dbias, dres, dw, db, None, None, None, None
             k.ln_bwd_row(dc, dy.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                          weight.data_ptr(), _lib.ptr(ds_in), ds.data_ptr(), dx.data_ptr(), rows, h,
                          float(ctx.p), ctx.key, _lib.stream())

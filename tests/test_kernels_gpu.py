@@ -27,7 +27,7 @@ def _gpu():
 
 
 # ---------------------------------------------------------------- LayerNorm
-@pytest.mark.parametrize("h", [1024, 4096, 2560])
+@pytest.mark.parametrize("h", [1024, 4096, 2560, 1408, 768, 1000, 4104])
 @pytest.mark.parametrize("fused", [False, True])
 def test_layer_norm_fwd_bwd(h, fused):
     from fleetx_amd import ops
@@ -69,6 +69,31 @@ def test_layer_norm_fwd_bwd(h, fused):
     if fused:
         assert _rel(bias.grad, biasr.grad) < 2e-2
         assert _rel(res.grad, resr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("rows,h", [(1000, 1408), (3, 1024), (16448, 768)])
+def test_ln_bwd_cols_uneven_rows(rows, h):
+    """The one-pass LayerNorm backward with column sums (ln_bwd_cols_kernel):
+    rows that leave the last waves short or empty, masked widths; dgamma,
+    dbeta and the fused bias gradient against fp32 torch."""
+    from fleetx_amd import ops
+    from fleetx_amd.ops import _lib
+    assert _lib.kernels().ln_bwd_cols_blocks(rows, h) > 0
+    x = torch.randn(rows, h, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(h, device=DEV)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(h, device=DEV)).bfloat16().requires_grad_()
+    bias = (0.1 * torch.randn(h, device=DEV)).bfloat16().requires_grad_()
+    res = torch.randn(rows, h, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    s, y = ops.add_layer_norm(x, bias, res, w, b, 1e-5, 0.0, 0)
+    xr, wr, br, biasr, resr = (t.detach().float().requires_grad_() for t in (x, w, b, bias, res))
+    sr = xr + biasr + resr
+    yr = torch.nn.functional.layer_norm(sr, (h,), wr, br, 1e-5)
+    gy, gs = torch.randn_like(yr), torch.randn_like(yr)
+    ((y.float() * gy).sum() + (s.float() * gs).sum()).backward()
+    ((yr * gy).sum() + (sr * gs).sum()).backward()
+    for got, ref in ((x.grad, xr.grad), (res.grad, resr.grad), (w.grad, wr.grad),
+                     (b.grad, br.grad), (bias.grad, biasr.grad)):
+        assert _rel(got, ref) < 2e-2
 
 
 # ---------------------------------------------------------------- GeLU / dropout
