@@ -79,7 +79,8 @@ int fx_softmax_fwd(int, int, const void*, const void*, void*, long, int, int, lo
                    hipStream_t);
 int fx_softmax_bwd(int, const void*, const void*, void*, long, int, int, float, int, hipStream_t);
 int fx_gemm(int, int, int, int, int, int, int, const void*, long, const void*, long, void*, long,
-            const void*, void*, long, int, hipStream_t, float*);
+            const void*, void*, long, int, hipStream_t, float*, float*);
+long fx_gemm_ws_bytes(int, int, int, int);
 void fx_gemm_set_variant(int);
 int fx_decode_gemv(int, int, int, int, int, const void*, long, const void*, long, const void*,
                    const void*, long, void*, long, void*, void*, const long*, int, int, int,
@@ -303,13 +304,14 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.def("gemm", [](int dt, int la, int lb, int epi, int M, int N, int K, ptr A, long lda, ptr B,
                    long ldb, ptr C, long ldc, ptr bias, ptr aux, long ldaux, int beta, ptr st,
-                   ptr sq) {
+                   ptr sq, ptr ws) {
     return fx_gemm(dt, la, lb, epi, M, N, K, CP(A), lda, CP(B), ldb, P(C), ldc, CP(bias), P(aux),
-                   ldaux, beta, S(st), F(sq));
+                   ldaux, beta, S(st), F(sq), F(ws));
   }, py::arg("dt"), py::arg("la"), py::arg("lb"), py::arg("epi"), py::arg("M"), py::arg("N"),
      py::arg("K"), py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("ldb"), py::arg("C"),
      py::arg("ldc"), py::arg("bias"), py::arg("aux"), py::arg("ldaux"), py::arg("beta"),
-     py::arg("st"), py::arg("sq") = 0);
+     py::arg("st"), py::arg("sq") = 0, py::arg("ws") = 0);
+  m.def("gemm_ws_bytes", &fx_gemm_ws_bytes);
   m.def("gemm_set_variant", &fx_gemm_set_variant);
   // decode-time skinny GEMM with fused sub-layer epilogues (decode_gemv.hip)
   m.def("decode_gemv", [](int dt, int epi, int M, int N, int K, ptr x, long ldx, ptr w, long ldw,

@@ -57,6 +57,7 @@ typedef short v4s __attribute__((ext_vector_type(4)));
 
 // gemm5.hip: the 4-wave kernel with the hand-scheduled K-loop
 int fx_gemm5_launch(int dt, int la, int lb, int epi, const fxg::GemmParams& P, hipStream_t st);
+long fx_gemm5_ws_bytes(int M, int N, int K);
 
 namespace {
 
@@ -1294,7 +1295,7 @@ extern "C" void fx_gemm_set_debug(unsigned long long* p) { g_dbg = p; }
 //   -4: an operand too large for 32-bit per-lane offsets.
 extern "C" int fx_gemm(int dt, int la, int lb, int epi, int M, int N, int K, const void* A,
                        long lda, const void* B, long ldb, void* C, long ldc, const void* bias,
-                       void* aux, long ldaux, int beta, hipStream_t st, float* sq) {
+                       void* aux, long ldaux, int beta, hipStream_t st, float* sq, float* ws) {
   if (M <= 0 || N <= 0 || K <= 0 || K % BK) return -1;
   if (sq != nullptr) {  // norm partials: the hand-scheduled kernel's fp32 epilogue only
     if (g_variant < 0) {
@@ -1328,5 +1329,17 @@ extern "C" int fx_gemm(int dt, int la, int lb, int epi, int M, int N, int K, con
   P.gm = g_gm > 0 ? g_gm : 8;
   P.dbg = g_dbg;
   P.sq = sq;
+  P.ws = epi == EPI_F32 ? ws : nullptr;
   return dt == 0 ? dispatch<bf16>(la, lb, epi, P, st) : dispatch<f16>(la, lb, epi, P, st);
+}
+
+// Split-K workspace (bytes) fx_gemm wants in `ws` for an fp32 weight-gradient
+// GEMM of this shape; 0 = it runs unsplit (gemm5.hip g5_split_plan).
+extern "C" long fx_gemm_ws_bytes(int epi, int M, int N, int K) {
+  if (g_variant < 0) {
+    const char* e = getenv("FLEETX_GEMM_PF");
+    g_variant = e ? atoi(e) : 5;
+  }
+  if (epi != EPI_F32 || g_variant != 5 || K < 2 * BK || K % BK) return 0;
+  return fx_gemm5_ws_bytes(M, N, K);
 }

@@ -31,6 +31,12 @@ struct GemmParams {
   // sq[4 * blockIdx.x + wave] -- the gradient-norm partials of a weight
   // gradient, taken from the accumulators instead of re-reading main_grad
   float* sq;
+  // EPI_F32 split-K (gemm5): this launch covers tiles [tile0, tile0 + gridDim.x / ksplit);
+  // with ksplit > 1 each tile's K range is cut into ksplit slices whose fp32
+  // partial tiles go to ws[(local tile * ksplit + slice) * TILE * TILE]
+  int tile0;
+  int ksplit;
+  float* ws;
 };
 
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {

@@ -68,6 +68,9 @@ def set_mode(mode):
 _DEFAULT_AUTO = "wgrad"
 AUTO_KINDS = set(k for k in os.environ.get("FLEETX_GEMM_AUTO", _DEFAULT_AUTO).split(",") if k)
 MIN_TILES = int(os.environ.get("FLEETX_GEMM_MIN_TILES", "192"))
+# weight gradients whose tiles underfill the chip run split along K
+# (gemm5.hip g5_split_plan), so they may take smaller shapes
+WGRAD_MIN_TILES = int(os.environ.get("FLEETX_GEMM_WGRAD_MIN_TILES", "64"))
 
 
 def _tiles(r, c, t=128):
@@ -95,7 +98,7 @@ def use(kind, a, b=None):
     if _MODE == "auto":
         if kind not in AUTO_KINDS or b is None:
             return False
-        return out_tiles(kind, a, b) >= MIN_TILES
+        return out_tiles(kind, a, b) >= (WGRAD_MIN_TILES if kind == "wgrad" else MIN_TILES)
     return True
 
 
@@ -110,10 +113,19 @@ def _ok(*ts):
 
 
 def _launch(dt, la, lb, epi, M, N, K, A, lda, B, ldb, C, ldc, bias=None, aux=None, ldaux=0,
-            beta=0, sq=None):
+            beta=0, sq=None, ws=None):
     return _lib.kernels().gemm(dt, la, lb, epi, M, N, K, A.data_ptr(), lda, B.data_ptr(), ldb,
                                C.data_ptr(), ldc, _lib.ptr(bias), _lib.ptr(aux), ldaux, int(beta),
-                               _lib.stream(), _lib.ptr(sq))
+                               _lib.stream(), _lib.ptr(sq), _lib.ptr(ws))
+
+
+def _splitk_ws(M, N, K, device):
+    """Scratch for the split-K slices of an fp32 weight-gradient GEMM whose
+    tiles do not fill whole waves of the chip (gemm5.hip ``g5_split_plan``:
+    the leftover tiles are cut along K and summed in slice order by a combine
+    launch); None when the shape runs unsplit."""
+    n = _lib.kernels().gemm_ws_bytes(EPI_F32, M, N, K)
+    return torch.empty(n // 4, device=device, dtype=torch.float32) if n else None
 
 
 def sq_slots(n, k):
@@ -204,7 +216,8 @@ def linear_wgrad(dy2, x2, out32, accumulate, sq=None):
     if sq is not None and (sq.dtype != torch.float32 or sq.numel() < sq_slots(N, K)):
         raise ValueError("linear_wgrad: sq needs {} fp32 slots".format(sq_slots(N, K)))
     rc = _launch(_lib.dt_code(dy2.dtype), LAY_MC, LAY_MC, EPI_F32, N, K, M, dy2, dy2.stride(0),
-                 x2, x2.stride(0), out32, K, beta=accumulate, sq=sq)
+                 x2, x2.stride(0), out32, K, beta=accumulate, sq=sq,
+                 ws=_splitk_ws(N, K, M, dy2.device))
     if rc == 0:
         _lib.maybe_sync()
     return rc == 0

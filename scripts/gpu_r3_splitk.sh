@@ -1,0 +1,35 @@
+#!/bin/bash
+# gemm5 split-K for fp32 weight gradients: GEMM tests; ViT-g and 345M / 1.3B
+# benches with split-K on / off and the wgrad tile threshold at 192 / 64;
+# 6.7B (no split shapes) as a guard; ViT-g and 345M traces.
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r3sk
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -v --tb=short --timeout 240 --timeout-method thread \
+  tests/test_gemm_gpu.py tests/test_fused_norm_gpu.py tests/test_model_parity_gpu.py > $O/pytest.log 2>&1
+rc=$?; echo "rc=$rc" >> $O/pytest.log; tail -4 $O/pytest.log; [ $rc -eq 0 ] || exit 1
+vit() {  # tag, env...
+  local t=$1; shift
+  env "$@" timeout -k 10 400 python tools/bench_vit.py --steps 8 --warmup 3 > $O/vit_$t.log 2>&1 || { tail -20 $O/vit_$t.log; exit 1; }
+  echo "vit $t $(tail -1 $O/vit_$t.log | grep -o '"value": [0-9.]*\|"mfu": [0-9.]*' | tr '\n' ' ')" | tee -a $O/summary.txt
+}
+gpt() {  # model, tag, env...
+  local m=$1 t=$2; shift 2
+  env "$@" timeout -k 10 400 python bench.py --model $m --steps 20 --warmup 3 > $O/gpt_${m}_$t.log 2>&1 || { tail -20 $O/gpt_${m}_$t.log; exit 1; }
+  echo "$m $t $(grep -o '"ms_per_step": [0-9.]*' $O/gpt_${m}_$t.log)" | tee -a $O/summary.txt
+}
+vit splitk FLEETX_GEMM5_SPLITK=1
+vit nosplit FLEETX_GEMM5_SPLITK=0
+vit splitk_min64 FLEETX_GEMM5_SPLITK=1 FLEETX_GEMM_WGRAD_MIN_TILES=64
+gpt gpt-345M splitk FLEETX_GEMM5_SPLITK=1
+gpt gpt-345M nosplit FLEETX_GEMM5_SPLITK=0
+gpt gpt-345M splitk_min64 FLEETX_GEMM5_SPLITK=1 FLEETX_GEMM_WGRAD_MIN_TILES=64
+gpt gpt3-1.3B splitk FLEETX_GEMM5_SPLITK=1
+gpt gpt3-1.3B nosplit FLEETX_GEMM5_SPLITK=0
+gpt gpt3-6.7B splitk FLEETX_GEMM5_SPLITK=1
+timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/prof_vit -o run -- python3 tools/bench_vit.py --steps 3 --warmup 2 > $O/prof_vit.log 2>&1 || { tail -5 $O/prof_vit.log; exit 1; }
+f=$(find $O/prof_vit -name "*kernel_trace.csv" | head -1)
+n=$(grep -c adamw_flat "$f"); per=$((n / 5))
+python3 tools/kernel_summary.py "$f" --window adamw_flat:$((2 * per)):$((5 * per)) --steps 3 --top 40 --md $O/kernels_vit_g.md > /dev/null
+gzip -f "$f"

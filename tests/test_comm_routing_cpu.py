@@ -43,10 +43,12 @@ def test_gemm_routing_table():
         # forward and data-gradient GEMMs stay on hipBLASLt by default
         assert not G.use("fwd", x, w_qkv) and not G.use("dgrad", t(8192, 12288), w_qkv)
         # hidden 1024-2048 shapes run on 128 x 128 tiles: 1.3B out-proj (256
-        # tiles), 345M qkv / fc1 (192 / 256); the 345M out-proj (64) under-fills
+        # tiles), 345M qkv / fc1 (192 / 256); the 345M out-proj (64 tiles) runs
+        # split along K (gemm5.hip g5_split_plan); 32 tiles stay on hipBLASLt
         assert G.use("wgrad", t(8192, 2048), t(8192, 2048))
         assert G.use("wgrad", t(8192, 3072), t(8192, 1024))
-        assert not G.use("wgrad", t(8192, 1024), t(8192, 1024))
+        assert G.use("wgrad", t(8192, 1024), t(8192, 1024))
+        assert not G.use("wgrad", t(8192, 512), t(8192, 1024))
         G.set_mode("blas")
         assert not G.use("wgrad", t(8192, 12288), x)
     finally:

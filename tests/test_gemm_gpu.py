@@ -134,6 +134,33 @@ def test_wgrad_norm_partials(gemm, M, N, K):
         gemm.linear_wgrad(dy, x, out, False, sq=sq[:8])
 
 
+@pytest.mark.parametrize("M,N,K", [(16448, 6144, 1408), (16448, 1408, 1408), (8192, 1024, 1024)])
+def test_wgrad_splitk(gemm, M, N, K):
+    """fp32 weight gradients whose tiles leave the last wave of the chip
+    mostly empty run their leftover tiles split along K (gemm5.hip
+    g5_split_plan; ViT-g FC1: 528 tiles on 512 slots -> 16 tiles x 32 slices)
+    and sum the slices in slice order: against fp32 torch for beta 0 / 1,
+    norm partials included, and bitwise repeatable."""
+    from fleetx_amd.ops import _lib
+    assert _lib.kernels().gemm_ws_bytes(gemm.EPI_F32, N, K, M) > 0
+    torch.manual_seed(7)
+    dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    ref = dy.float().t() @ x.float()
+    base = torch.randn(N, K, device="cuda", dtype=torch.float32)
+    out = base.clone()
+    sq = torch.zeros(gemm.sq_slots(N, K), device="cuda")
+    assert gemm.linear_wgrad(dy, x, out, True, sq=sq)
+    assert _rel(out, base + ref) < 1e-4
+    assert abs(float(sq.double().sum()) - float(out.double().pow(2).sum())) < 1e-5 * float(out.double().pow(2).sum())
+    out2 = torch.empty_like(out)
+    assert gemm.linear_wgrad(dy, x, out2, False)
+    assert _rel(out2, ref) < 1e-4
+    out3 = torch.empty_like(out)
+    assert gemm.linear_wgrad(dy, x, out3, False)
+    assert torch.equal(out2, out3)
+
+
 def test_strided_rows(gemm):
     """Row-strided activations (a column slice of a wider buffer) are read in place."""
     torch.manual_seed(5)

@@ -8,7 +8,7 @@
 #include <string.h>
 
 extern "C" int fx_gemm(int, int, int, int, int, int, int, const void*, long, const void*, long,
-                       void*, long, const void*, void*, long, int, hipStream_t);
+                       void*, long, const void*, void*, long, int, hipStream_t, float*, float*);
 extern "C" void fx_gemm_set_variant(int);
 extern "C" void fx_gemm_set_debug(unsigned long long*);
 
@@ -64,7 +64,7 @@ int main(int argc, char** argv) {
       }
       auto run = [&]() {
         int rc = fx_gemm(0, c.la, c.lb, c.epi, c.m, c.n, c.k, c.A, c.lda, c.B, c.ldb, c.C, c.ldc,
-                         nullptr, aux, c.n, 1, 0);
+                         nullptr, aux, c.n, 1, 0, nullptr, nullptr);
         if (rc) { printf("rc %d\n", rc); exit(1); }
       };
       for (int i = 0; i < 3; ++i) run();
