@@ -152,6 +152,12 @@ class EagerEngine(BasicEngine):
         self._nan_guard = e.get("nan_guard", "off")
         self._metrics_file = e.get("metrics_file") or os.environ.get("FLEETX_METRICS_FILE")
         self._fault = os.environ.get("FLEETX_FAULT_INJECT")  # "rank:step" -> os._exit(17)
+        # GEMM kinds on the MFMA kernel under FLEETX_GEMM=auto, per model
+        # (the env var FLEETX_GEMM_AUTO wins): e.g. ViT-g's data gradients
+        routing = e.get("gemm_routing")
+        if routing and "FLEETX_GEMM_AUTO" not in os.environ:
+            from ...ops import gemm as _gemm
+            _gemm.set_auto_kinds(routing)
 
         self.hcg = topo.get_hcg()
         self._dp_rank = self.hcg.dp_rank

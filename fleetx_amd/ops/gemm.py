@@ -73,6 +73,14 @@ MIN_TILES = int(os.environ.get("FLEETX_GEMM_MIN_TILES", "192"))
 WGRAD_MIN_TILES = int(os.environ.get("FLEETX_GEMM_WGRAD_MIN_TILES", "64"))
 
 
+def set_auto_kinds(kinds):
+    """Replace the kinds routed under ``auto`` ('wgrad,dgrad' or a list)."""
+    if isinstance(kinds, str):
+        kinds = [k.strip() for k in kinds.split(",")]
+    AUTO_KINDS.clear()
+    AUTO_KINDS.update(k for k in kinds if k)
+
+
 def _tiles(r, c, t=128):
     return ((r + t - 1) // t) * ((c + t - 1) // t)
 
