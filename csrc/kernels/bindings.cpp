@@ -18,7 +18,7 @@ void fx_add_ln_fwd(int, const void*, const void*, const void*, const void*, cons
                    void*, float*, float*, int, int, float, float, uint64_t, hipStream_t);
 void fx_ln_bwd_row(int, const void*, const void*, const float*, const float*, const void*,
                    const void*, void*, void*, int, int, float, uint64_t, hipStream_t);
-int fx_ln_bwd_cols_blocks(int, int);
+int fx_ln_bwd_cols_blocks(int, int, int);
 int fx_ln_bwd_cols(int, const void*, const void*, const float*, const float*, const void*,
                    const void*, void*, void*, int, int, float, uint64_t, float*, int, float*, void*,
                    int, float*, void*, int, float*, void*, int, hipStream_t);

@@ -299,106 +299,115 @@ __global__ __launch_bounds__(256) void ln_bwd_row_generic(
 }
 
 // ---------------------------------------------------------------------------
-// Row backward + its column sums in one pass (h <= 1536):
+// Row backward + its column sums in one pass (h <= 4096):
 //   ds = ds_in + LN'(dy),  dx = dropout'(ds)          (as ln_bwd_row_kernel)
 //   dgamma = sum dy * xhat,  dbeta = sum dy,  dbias = sum dx (optional: the
 //   bias of the linear that feeds the fused residual add)
 // instead of the row kernel + two column-tile passes that re-read dy and s
-// (reference K07's LayerNorm backward + the bias gradient of K09).  Each wave
-// owns a contiguous run of rows, keeps its columns' sums in registers and
-// loads the next row while it reduces the current one; gamma is read once
-// per wave.  The 4 waves' sums meet in LDS in a fixed order and the block
-// writes one partial row per array ([3][G][h] fp32); ln_cols_finalize_kernel
-// adds the G rows in a fixed order -- bitwise reproducible.
+// (reference K07's LayerNorm backward + the bias gradient of K09).  A row is
+// WPR waves wide (1 / 2 / 4 for h <= 1536 / 3072 / 4096: each wave owns a
+// slice of the columns and the row sums meet in LDS); each row group owns a
+// contiguous run of rows and keeps its columns' sums in registers.  Register
+// budget (<= 3 vectors per lane, two waves per SIMD; 4 spilled): gamma stays
+// packed, and xhat / dy are re-derived from the packed row in the second
+// pass instead of being held as floats.
+// The row groups' sums meet in LDS in a fixed order and the block writes one
+// partial row per array ([3][G][h] fp32); ln_cols_finalize_kernel adds the G
+// rows in a fixed order -- bitwise reproducible.
 // ---------------------------------------------------------------------------
-template <typename T, int VPT, bool MASK, bool DB>
-__global__ __launch_bounds__(256) void ln_bwd_cols_kernel(
+template <typename T, int VPT, int WPR, bool MASK, bool DB>
+__global__ __launch_bounds__(256, 2) void ln_bwd_cols_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ s,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const uint16_t* __restrict__ gamma, const uint16_t* __restrict__ ds_in,
     uint16_t* __restrict__ ds_out, uint16_t* __restrict__ dx_out, int rows, int h,
-    int rows_per_wave, float* __restrict__ part, DropCfg drop_) {
-  __shared__ float red[4 * 512 * VPT];
+    int rows_per_group, float* __restrict__ part, DropCfg drop_) {
+  constexpr int NG = 4 / WPR;                 // row groups per block
+  __shared__ float red[4 * 512 * VPT];        // NG groups x h columns
+  __shared__ float xs[2][4][2];               // WPR > 1: the waves' row sums, by row parity
   const DropCfg drop = resolve_drop(drop_);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r0 = min(rows, (blockIdx.x * 4 + w) * rows_per_wave);
-  const int r1 = min(rows, r0 + rows_per_wave);
-  float g[VPT][8], ag[VPT][8], ab[VPT][8], ax[DB ? VPT : 1][8];
+  const int grp = w / WPR, half = w % WPR;
+  const int hw = h / WPR, cbase = half * hw;
+  const int r0 = min(rows, (blockIdx.x * NG + grp) * rows_per_group);
+  const int r1 = min(rows, r0 + rows_per_group);
+  uint4 gp[VPT];
+  float ag[VPT][8], ab[VPT][8], ax[DB ? VPT : 1][8];
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int c = (i * 64 + lane) * 8;
-    if (!MASK || c < h) {
-      load8<T>(gamma + c, g[i]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) g[i][j] = 0.f;
-    }
+    gp[i] = (!MASK || c < hw) ? *reinterpret_cast<const uint4*>(gamma + cbase + c)
+                              : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       ag[i][j] = ab[i][j] = 0.f;
       if (DB) ax[i][j] = 0.f;
     }
   }
-  // next-row prefetch only where the registers allow two waves per SIMD
-  constexpr bool PF = VPT <= 2;
-  uint4 na[VPT], nd[VPT], nr[VPT];
-  auto fetch = [&](int r) {
-    const size_t base = (size_t)r * h;
-#pragma unroll
-    for (int i = 0; i < VPT; ++i) {
-      const int c = (i * 64 + lane) * 8;
-      if (MASK && c >= h) continue;
-      na[i] = *reinterpret_cast<const uint4*>(s + base + c);
-      nd[i] = *reinterpret_cast<const uint4*>(dy + base + c);
-      if (ds_in) nr[i] = *reinterpret_cast<const uint4*>(ds_in + base + c);
-    }
-  };
-  if (PF && r0 < r1) fetch(r0);
-  for (int r = r0; r < r1; ++r) {
-    if (!PF) fetch(r);
+  for (int k = 0; k < rows_per_group; ++k) {
+    const int r = r0 + k;
+    const bool live = r < r1;   // WPR > 1: every wave runs every iteration (LDS barrier)
+    if (WPR == 1 && !live) break;
+    const size_t base = (size_t)(live ? r : 0) * h + cbase;
     uint4 ca[VPT], cd[VPT], cr[VPT];
+    float mean = 0.f, rstd = 0.f, s1 = 0.f, s2 = 0.f;
+    if (live) {
 #pragma unroll
-    for (int i = 0; i < VPT; ++i) {
-      ca[i] = na[i];
-      cd[i] = nd[i];
-      cr[i] = nr[i];
+      for (int i = 0; i < VPT; ++i) {
+        const int c = (i * 64 + lane) * 8;
+        if (MASK && c >= hw) continue;
+        ca[i] = *reinterpret_cast<const uint4*>(s + base + c);
+        cd[i] = *reinterpret_cast<const uint4*>(dy + base + c);
+        if (ds_in) cr[i] = *reinterpret_cast<const uint4*>(ds_in + base + c);
+      }
+      mean = mean_in[r];
+      rstd = rstd_in[r];
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) {
+        const int c = (i * 64 + lane) * 8;
+        if (MASK && c >= hw) continue;
+        float a[8], d[8], g[8];
+        unpack8<T>(ca[i], a);
+        unpack8<T>(cd[i], d);
+        unpack8<T>(gp[i], g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (a[j] - mean) * rstd, gd = d[j] * g[j];
+          s1 += gd;
+          s2 += gd * xh;
+          ag[i][j] += d[j] * xh;
+          ab[i][j] += d[j];
+        }
+      }
     }
-    if (PF && r + 1 < r1) fetch(r + 1);
-    const size_t base = (size_t)r * h;
-    const float mean = mean_in[r], rstd = rstd_in[r];
-    float xh[VPT][8], dd[VPT][8];
-    float s1 = 0.f, s2 = 0.f;
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if constexpr (WPR > 1) {
+      if (lane == 0) {
+        xs[k & 1][w][0] = s1;
+        xs[k & 1][w][1] = s2;
+      }
+      __syncthreads();
+      s1 = xs[k & 1][WPR * grp][0];
+      s2 = xs[k & 1][WPR * grp][1];
+#pragma unroll
+      for (int q = 1; q < WPR; ++q) {
+        s1 += xs[k & 1][WPR * grp + q][0];
+        s2 += xs[k & 1][WPR * grp + q][1];
+      }
+    }
+    if (!live) continue;
+    const float m1 = s1 / h, m2 = s2 / h;
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
       const int c = (i * 64 + lane) * 8;
-      if (MASK && c >= h) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) xh[i][j] = dd[i][j] = 0.f;
-        continue;
-      }
-      float a[8];
+      if (MASK && c >= hw) continue;
+      float a[8], d[8], g[8], o[8];
       unpack8<T>(ca[i], a);
-      unpack8<T>(cd[i], dd[i]);
+      unpack8<T>(cd[i], d);
+      unpack8<T>(gp[i], g);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        xh[i][j] = (a[j] - mean) * rstd;
-        const float gd = dd[i][j] * g[i][j];
-        s1 += gd;
-        s2 += gd * xh[i][j];
-      }
-    }
-    const float m1 = wave_sum(s1) / h, m2 = wave_sum(s2) / h;
-#pragma unroll
-    for (int i = 0; i < VPT; ++i) {
-      const int c = (i * 64 + lane) * 8;
-      if (MASK && c >= h) continue;
-      float o[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        o[j] = rstd * (dd[i][j] * g[i][j] - m1 - xh[i][j] * m2);
-        ag[i][j] += dd[i][j] * xh[i][j];
-        ab[i][j] += dd[i][j];
-      }
+      for (int j = 0; j < 8; ++j) o[j] = rstd * (d[j] * g[j] - m1 - (a[j] - mean) * rstd * m2);
       if (ds_in) {
         float rr[8];
         unpack8<T>(cr[i], rr);
@@ -419,22 +428,26 @@ __global__ __launch_bounds__(256) void ln_bwd_cols_kernel(
       }
     }
   }
-  // block partials: the 4 waves' column sums, added in wave order
+  // block partials: the row groups' column sums, added in group order
 #pragma unroll
   for (int arr = 0; arr < (DB ? 3 : 2); ++arr) {
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
       const int c = (i * 64 + lane) * 8;
-      if (MASK && c >= h) continue;
+      if (MASK && c >= hw) continue;
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        red[w * h + c + j] = arr == 0 ? ag[i][j] : arr == 1 ? ab[i][j] : ax[DB ? i : 0][j];
+        red[grp * h + cbase + c + j] = arr == 0 ? ag[i][j] : arr == 1 ? ab[i][j] : ax[DB ? i : 0][j];
     }
     __syncthreads();
     float* out = part + ((size_t)arr * gridDim.x + blockIdx.x) * h;
-    for (int c = threadIdx.x; c < h; c += 256)
-      out[c] = ((red[c] + red[h + c]) + red[2 * h + c]) + red[3 * h + c];
+    for (int c = threadIdx.x; c < h; c += 256) {
+      float v = red[c];
+#pragma unroll
+      for (int q = 1; q < NG; ++q) v += red[q * h + c];
+      out[c] = v;
+    }
   }
 }
 
@@ -967,16 +980,24 @@ extern "C" void fx_ln_bwd_row(int dtype, const void* dy, const void* s, const fl
 #undef LNB_CASE
 }
 
-// Fused LayerNorm backward (h % 8 == 0, h <= 1536): rows per wave and
-// partial rows G for a given row count (the caller sizes part = [3][G][h]).
-static int ln_cols_rows_per_wave(int rows) {
-  int rpw = (rows + 512 * 4 - 1) / (512 * 4);
-  return rpw < 2 ? 2 : rpw;
+// Fused LayerNorm backward (h <= 4096): waves per row, rows per row group
+// and partial rows G (the caller sizes part = [3][G][h]).
+static int ln_cols_wpr(int h) { return h <= 1536 ? 1 : h <= 3072 ? 2 : 4; }
+static int ln_cols_rows_per_group(int rows, int h) {
+  const int ng = 4 / ln_cols_wpr(h);
+  int rpg = (rows + 512 * ng - 1) / (512 * ng);
+  return rpg < 2 ? 2 : rpg;
 }
-extern "C" int fx_ln_bwd_cols_blocks(int rows, int h) {
-  if (h % 8 || h > 1536 || rows <= 0) return 0;   // <= 3 vectors per lane: 2 waves / SIMD
-  const int rpw = ln_cols_rows_per_wave(rows);
-  return (rows + 4 * rpw - 1) / (4 * rpw);
+// max_h: the caller's width limit (fleetx_amd/ops/norm.py, FLEETX_LN_BWD_FUSED:
+// 1536 = one wave per row, the default; 4096 = also 2 / 4 waves per row).
+// Measured (profiles/r3_colsum/wide_rows.txt): at h 4096 the per-row LDS
+// barrier of 4 waves makes the pass 76-109 us against 60 us for the row
+// kernel, more than the column passes it saves (7.75 vs 7.38 ms per 6.7B
+// step); h 2048 is neutral.
+extern "C" int fx_ln_bwd_cols_blocks(int rows, int h, int max_h) {
+  if (rows <= 0 || h > (max_h < 4096 ? max_h : 4096) || h % (8 * ln_cols_wpr(h))) return 0;
+  const int ng = 4 / ln_cols_wpr(h), rpg = ln_cols_rows_per_group(rows, h);
+  return (rows + ng * rpg - 1) / (ng * rpg);
 }
 
 // Returns 0 when launched, -1 when the shape is not covered.
@@ -986,9 +1007,10 @@ extern "C" int fx_ln_bwd_cols(int dtype, const void* dy, const void* s, const fl
                               float* part, int with_dbias, float* fg, void* tg, int accg,
                               float* fb, void* tb, int accb, float* fx, void* tx, int accx,
                               hipStream_t st) {
-  const int G = fx_ln_bwd_cols_blocks(rows, h);
+  const int G = fx_ln_bwd_cols_blocks(rows, h, 4096);
   if (G == 0) return -1;
-  const int rpw = ln_cols_rows_per_wave(rows);
+  const int wpr = ln_cols_wpr(h), hw = h / wpr;
+  const int rpg = ln_cols_rows_per_group(rows, h);
   DropCfg d = make_drop(p, key);
   auto DY = (const uint16_t*)dy;
   auto S = (const uint16_t*)s;
@@ -996,24 +1018,27 @@ extern "C" int fx_ln_bwd_cols(int dtype, const void* dy, const void* s, const fl
   auto DI = (const uint16_t*)ds_in;
   auto DS = (uint16_t*)ds_out;
   auto DX = (uint16_t*)dx_out;
-  const int vpt = (h + 511) / 512;
-  const bool mask = h % 512 != 0;
-#define LNC_GO(V, M, DB)                                                                      \
-  FX_DISPATCH_T(dtype, ln_bwd_cols_kernel<T, V, M, DB><<<G, 256, 0, st>>>(                    \
-                           DY, S, mean, rstd, GM, DI, DS, DX, rows, h, rpw, part, d))
+  const int vpt = (hw + 511) / 512;
+  const bool mask = hw % 512 != 0;
+#define LNC_GO(V, W, M, DB)                                                                   \
+  FX_DISPATCH_T(dtype, ln_bwd_cols_kernel<T, V, W, M, DB><<<G, 256, 0, st>>>(                 \
+                           DY, S, mean, rstd, GM, DI, DS, DX, rows, h, rpg, part, d))
+#define LNC_M(V, W)                                                                           \
+  if (mask) {                                                                                 \
+    if (with_dbias) { LNC_GO(V, W, true, true); } else { LNC_GO(V, W, true, false); }         \
+  } else {                                                                                    \
+    if (with_dbias) { LNC_GO(V, W, false, true); } else { LNC_GO(V, W, false, false); }       \
+  }
 #define LNC_V(V)                                                                              \
   case V:                                                                                     \
-    if (mask) {                                                                               \
-      if (with_dbias) { LNC_GO(V, true, true); } else { LNC_GO(V, true, false); }             \
-    } else {                                                                                  \
-      if (with_dbias) { LNC_GO(V, false, true); } else { LNC_GO(V, false, false); }           \
-    }                                                                                         \
+    if (wpr == 1) { LNC_M(V, 1) } else if (wpr == 2) { LNC_M(V, 2) } else { LNC_M(V, 4) }     \
     break;
   switch (vpt) {
     LNC_V(1) LNC_V(2) LNC_V(3)
     default: return -1;
   }
 #undef LNC_V
+#undef LNC_M
 #undef LNC_GO
   LnColsOut f;
   f.f32[0] = fg; f.f32[1] = fb; f.f32[2] = fx;

@@ -131,8 +131,13 @@ def _dropout_ref(x, p, key):
     return torch.where(m, x * (1.0 / (1.0 - p)), torch.zeros_like(x))
 
 
-# FLEETX_LN_BWD_FUSED=0 keeps the row kernel + column-tile passes (A/B)
-_LN_BWD_COLS = os.environ.get("FLEETX_LN_BWD_FUSED", "1") != "0"
+def _ln_bwd_cols_max_h():
+    """Widest LayerNorm the one-pass backward takes: FLEETX_LN_BWD_FUSED=0
+    keeps the row kernel + column-tile passes everywhere, 1 (default) uses
+    it up to h 1536 (one wave per row), 2 up to 4096 (2 / 4 waves per row:
+    measured slower at 4096, neutral at 2048 -- profiles/r3_colsum/)."""
+    mode = os.environ.get("FLEETX_LN_BWD_FUSED", "1")
+    return {"0": 0, "2": 4096}.get(mode, 1536)
 
 
 def _main_grad_target(p):
@@ -145,7 +150,7 @@ def _ln_bwd_cols(k, dc, dy, s, mean, rstd, weight, ctx, ds_in, ds, dx, rows, h):
     small finalize launch (csrc/kernels/norm_eltwise.hip ``ln_bwd_cols_kernel``)
     -- written into the fp32 ``main_grad`` where the parameter has one, else
     returned as 16-bit gradients."""
-    G = k.ln_bwd_cols_blocks(rows, h)
+    G = k.ln_bwd_cols_blocks(rows, h, 4096)
     with_db = bool(ctx.has_bias)
     part = torch.empty(3 if with_db else 2, G, h, device=dy.device, dtype=torch.float32)
     outs, grads, done = [], [], []
@@ -234,7 +239,7 @@ class _AddLayerNorm(torch.autograd.Function):
             dc = _lib.dt_code(dy.dtype)
             ds = torch.empty_like(dy)
             dx = torch.empty_like(dy) if ctx.p > 0 else ds
-            if _LN_BWD_COLS and k.ln_bwd_cols_blocks(rows, h) > 0:
+            if k.ln_bwd_cols_blocks(rows, h, _ln_bwd_cols_max_h()) > 0:
                 dw, db, dbias = _ln_bwd_cols(k, dc, dy, s, mean, rstd, weight, ctx, ds_in, ds, dx,
                                              rows, h)
                 dres = ds if ctx.has_res else None

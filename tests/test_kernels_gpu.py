@@ -71,14 +71,15 @@ def test_layer_norm_fwd_bwd(h, fused):
         assert _rel(res.grad, resr.grad) < 2e-2
 
 
-@pytest.mark.parametrize("rows,h", [(1000, 1408), (3, 1024), (16448, 768)])
-def test_ln_bwd_cols_uneven_rows(rows, h):
+@pytest.mark.parametrize("rows,h", [(1000, 1408), (3, 1024), (16448, 768), (1000, 4096), (7, 2048), (513, 2560)])
+def test_ln_bwd_cols_uneven_rows(rows, h, monkeypatch):
     """The one-pass LayerNorm backward with column sums (ln_bwd_cols_kernel):
     rows that leave the last waves short or empty, masked widths; dgamma,
     dbeta and the fused bias gradient against fp32 torch."""
     from fleetx_amd import ops
     from fleetx_amd.ops import _lib
-    assert _lib.kernels().ln_bwd_cols_blocks(rows, h) > 0
+    monkeypatch.setenv("FLEETX_LN_BWD_FUSED", "2")   # 2 / 4 waves per row for h > 1536
+    assert _lib.kernels().ln_bwd_cols_blocks(rows, h, 4096) > 0
     x = torch.randn(rows, h, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     w = (1 + 0.1 * torch.randn(h, device=DEV)).bfloat16().requires_grad_()
     b = (0.1 * torch.randn(h, device=DEV)).bfloat16().requires_grad_()
