@@ -209,7 +209,10 @@ class GPTDecoderLayer(nn.Module):
             # the out-proj bias is a leaf: pass it around the checkpoint, not through it
             a, ab = recompute(self._attn_block_out, x), self.attn.out_proj.bias
         else:
-            a, ab = self._attn_block(x)
+            # LN1 hands back x as the residual alias: the residual branch's
+            # gradient joins the LN1 backward kernel (no separate add pass)
+            x, h1 = ops.layer_norm_keep_input(x, self.ln1.weight, self.ln1.bias, self.ln1.eps)
+            a, ab = self.attn(h1)
         k1 = _key(stream) if p > 0 else 0
         x2, h2 = ops.add_layer_norm(a, ab, x, self.ln2.weight, self.ln2.bias, self.ln2.eps, p, k1)
         m, mb = self.mlp(h2)

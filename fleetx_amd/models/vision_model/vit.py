@@ -153,7 +153,11 @@ class Block(nn.Module):
             # residual + proj bias + LN2 in one kernel, FFN1+GeLU(erf)+FFN2 as one
             # autograd node, residual + FFN2 bias in one kernel; every weight and
             # bias gradient lands in fp32 main_grad (same blocks as the GPT layer)
-            a, ab = self.attn.forward_nobias(self.norm1(x))
+            # x comes back as the residual alias: its two branch gradients meet
+            # inside the LN1 backward kernel (no separate add pass)
+            x, h1 = ops.layer_norm_keep_input(x, self.norm1.weight, self.norm1.bias,
+                                              self.norm1.eps)
+            a, ab = self.attn.forward_nobias(h1)
             x2, h2 = ops.add_layer_norm(a, ab, x, self.norm2.weight, self.norm2.bias,
                                         self.norm2.eps)
             m = fused_mlp(h2, self.mlp.fc1.weight, self.mlp.fc1.bias, self.mlp.fc2.weight,

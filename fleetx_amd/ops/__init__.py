@@ -1,5 +1,5 @@
 """Hot-path ops: HIP/CDNA4 kernels on GPU tensors, reference math on CPU."""
-from .norm import add_layer_norm, layer_norm, FusedLayerNorm, col_sum  # noqa: F401
+from .norm import add_layer_norm, layer_norm, layer_norm_keep_input, FusedLayerNorm, col_sum  # noqa: F401
 from .elementwise import bias_gelu, bias_dropout_add, dropout  # noqa: F401
 from .attention import (flash_attention, flash_attention_qkvpacked, attention_reference,  # noqa: F401
                         decode_attention)

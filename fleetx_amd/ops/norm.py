@@ -191,7 +191,8 @@ class _AddLayerNorm(torch.autograd.Function):
         if x.is_cuda:
             k = _lib.kernels()
             x = x.contiguous()
-            fused = store_sum or bias is not None or residual is not None or p > 0
+            fused = bias is not None or residual is not None or p > 0
+            # store_sum with nothing to add: s IS x (returned as an alias, no copy)
             s = torch.empty_like(x) if fused else None
             y = torch.empty_like(x)
             mean = torch.empty(rows, device=x.device, dtype=torch.float32)
@@ -201,6 +202,8 @@ class _AddLayerNorm(torch.autograd.Function):
                          mean.data_ptr(), rstd.data_ptr(), rows, h, float(eps), float(p), key,
                          _lib.stream())
             s_saved = s if s is not None else x
+            if s is None and store_sum:
+                s = x
         else:
             v = x if bias is None else x + bias
             v = _dropout_ref(v, p, key)
@@ -283,6 +286,17 @@ def add_layer_norm(x, bias, residual, weight, lnbias, eps=1e-5, p=0.0, key=0):
 
 def layer_norm(x, weight, bias, eps=1e-5):
     return _AddLayerNorm.apply(x, None, None, weight, bias, eps, 0.0, 0, False)
+
+
+def layer_norm_keep_input(x, weight, bias, eps=1e-5):
+    """``(x', LN(x))`` with ``x'`` an alias of ``x`` to use as the residual:
+    the gradient that reaches ``x'`` enters the LayerNorm backward kernel as
+    its ``ds_in`` instead of autograd adding the two branch gradients of
+    ``x`` in a separate pass (pre-LN blocks: ``x + f(LN(x))``).
+    ``FLEETX_LN_KEEP_INPUT=0``: plain LayerNorm (A/B)."""
+    if os.environ.get("FLEETX_LN_KEEP_INPUT", "1") == "0":
+        return x, layer_norm(x, weight, bias, eps)
+    return _AddLayerNorm.apply(x, None, None, weight, bias, eps, 0.0, 0, True)
 
 
 class FusedLayerNorm(torch.nn.Module):
