@@ -607,7 +607,35 @@ __global__ __launch_bounds__(256) void coltile_partial_kernel(
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc0[j] = acc1[j] = 0.f;
   if (col < cols) {
-    for (int r = r0 + ty; r < r1; r += 16) {
+    // 4 rows' loads in flight per thread (the loop-carried adds otherwise
+    // leave one row's latency exposed per iteration); added in row order
+    int r = r0 + ty;
+    for (; r + 48 < r1; r += 64) {
+      float va[4][8], vb[MODE == 0 ? 4 : 1][8], m[4], rs[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const size_t off = (size_t)(r + 16 * q) * cols + col;
+        load8<T>(a + off, va[q]);
+        if (MODE == 0) {
+          load8<T>(b + off, vb[q]);
+          m[q] = mean[r + 16 * q];
+          rs[q] = rstd[r + 16 * q];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (MODE == 0) {
+            acc0[j] += va[q][j] * (vb[MODE == 0 ? q : 0][j] - m[q]) * rs[q];
+            acc1[j] += va[q][j];
+          } else {
+            acc0[j] += va[q][j];
+          }
+        }
+      }
+    }
+    for (; r < r1; r += 16) {
       const size_t off = (size_t)r * cols + col;
       float va[8];
       load8<T>(a + off, va);
@@ -786,7 +814,26 @@ __global__ __launch_bounds__(256) void dropout_bwd_colsum_kernel(
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
   if (col < cols) {
-    for (int r = r0 + ty; r < r1; r += 16) {
+    int r = r0 + ty;
+    for (; r + 48 < r1; r += 64) {  // 4 rows' loads in flight, added in row order
+      float g[4][8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) load8<T>(dout + (size_t)(r + 16 * q) * cols + col, g[q]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const size_t off = (size_t)(r + 16 * q) * cols + col;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[q][j] = drop_apply(g[q][j], off + j, drop);
+        if (dx) {
+          store8<T>(dx + off, g[q]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[q][j] = round_to<T>(g[q][j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += g[q][j];
+      }
+    }
+    for (; r < r1; r += 16) {
       const size_t off = (size_t)r * cols + col;
       float g[8];
       load8<T>(dout + off, g);
