@@ -184,3 +184,21 @@ def test_fused_lm_head_ce_matches_plain_head(tmp_path, micro, monkeypatch):
     assert torch.allclose(p0, p1, rtol=1e-5, atol=1e-6), float((p0 - p1).abs().max())
     from fleetx_amd.ops import lm_head_ce
     lm_head_ce.check()  # the declared gradient matched every backward
+
+
+def test_engine_gemm_routing_key(tmp_path, monkeypatch):
+    """``Engine.gemm_routing`` sets the GEMM kinds routed to the MFMA kernel
+    under FLEETX_GEMM=auto (the ViT-g config routes data gradients too); an
+    explicit FLEETX_GEMM_AUTO in the environment wins."""
+    from fleetx_amd.ops import gemm as G
+    old = set(G.AUTO_KINDS)
+    try:
+        monkeypatch.delenv("FLEETX_GEMM_AUTO", raising=False)
+        _engine(tmp_path / "a", ["Engine.gemm_routing=wgrad,dgrad"])
+        assert G.AUTO_KINDS == {"wgrad", "dgrad"}
+        G.set_auto_kinds(old)
+        monkeypatch.setenv("FLEETX_GEMM_AUTO", "wgrad")
+        _engine(tmp_path / "b", ["Engine.gemm_routing=wgrad,dgrad,fwd"])
+        assert G.AUTO_KINDS == old
+    finally:
+        G.set_auto_kinds(old)
