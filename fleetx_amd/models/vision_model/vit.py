@@ -46,6 +46,9 @@ def _fused_grads(lin):
     """Let the linear's weight / bias gradients go straight into the flat fp32
     ``main_grad`` buffer (parallel/linear.py, ops/norm.py)."""
     lin.weight._fx_fused_wgrad_ok = True
+    # its gradient comes from the wgrad GEMM: the epilogue's sums of squares
+    # feed the global gradient norm (grad_buffer.enable_fused_norm)
+    lin.weight._fx_gemm_wgrad = True
     if lin.bias is not None:
         lin.bias._fx_fused_wgrad_ok = True
     return lin

@@ -288,8 +288,10 @@ class FusedAdamW(FlatOptimizer):
         # profiles/r2_final/adamw_overlap_grid.txt).  0 = uncapped.
         grid = int(os.environ.get("FLEETX_ADAMW_OVERLAP_GRID", str(self.overlap_grid)))
         wide = int(os.environ.get("FLEETX_ADAMW_OVERLAP_WIDE", str(int(self.overlap_wide))))
-        if grid:
-            k.adamw_tune(grid, 1, wide)
+        # the root unit (embeddings) and layer 0 gate the first forward kernel:
+        # nothing else can run yet, so they take the whole chip; the cap starts
+        # with layer 1 (FLEETX_ADAMW_OVERLAP_HEAD=0: capped from the start)
+        head = int(os.environ.get("FLEETX_ADAMW_OVERLAP_HEAD", "2"))
         if getattr(self, "_overlap_args", None) is None:
             # launch arguments per unit, built once (the flat buffers never
             # move): the per-step host cost is then one bound call per range
@@ -315,7 +317,9 @@ class FusedAdamW(FlatOptimizer):
         b1, b2, eps = self.beta1, self.beta2, self.eps
         with torch.cuda.stream(os_):
             st = _lib.stream()
-            for u, args in self._overlap_args:
+            for i, (u, args) in enumerate(self._overlap_args):
+                if grid and i == head:
+                    k.adamw_tune(grid, 1, wide)
                 for mp, gp, m1, v1, pp, n, wd in args:
                     adamw(dt, mp, gp, m1, v1, pp, n, lr, b1, b2, eps, wd, 0.0, gs, fi, ds, st)
                 ev = torch.cuda.Event()
