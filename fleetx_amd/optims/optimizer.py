@@ -288,10 +288,11 @@ class FusedAdamW(FlatOptimizer):
         # profiles/r2_final/adamw_overlap_grid.txt).  0 = uncapped.
         grid = int(os.environ.get("FLEETX_ADAMW_OVERLAP_GRID", str(self.overlap_grid)))
         wide = int(os.environ.get("FLEETX_ADAMW_OVERLAP_WIDE", str(int(self.overlap_wide))))
-        # the root unit (embeddings) and layer 0 gate the first forward kernel:
-        # nothing else can run yet, so they take the whole chip; the cap starts
-        # with layer 1 (FLEETX_ADAMW_OVERLAP_HEAD=0: capped from the start)
-        head = int(os.environ.get("FLEETX_ADAMW_OVERLAP_HEAD", "2"))
+        # FLEETX_ADAMW_OVERLAP_HEAD=n: the first n units (root = embeddings,
+        # then layer 0, ...) run uncapped, as they gate the first forward
+        # kernels; measured neutral on 6.7B / 1.3B (profiles/r3_adamw/
+        # head_ab.txt), so capped from the start by default
+        head = int(os.environ.get("FLEETX_ADAMW_OVERLAP_HEAD", "0"))
         if getattr(self, "_overlap_args", None) is None:
             # launch arguments per unit, built once (the flat buffers never
             # move): the per-step host cost is then one bound call per range
