@@ -237,6 +237,7 @@ struct AttnParams {
   int dval;              // valid head dim (<= the tile's D; columns past it are zero)
   int delta_in_dq;       // backward: the dQ pass computes and stores delta (no pre-pass)
   const uint64_t* salt;  // graph mode: per-replay device salt (fx_set_dropout_salt)
+  int full_tiles;        // forward: compute fully masked key halves too (A/B, FLEETX_FA_HALF_SKIP=0)
 };
 
 // per-(batch, head) dropout hash seed; under graph mode the baked key is
@@ -305,15 +306,25 @@ __device__ __forceinline__ void fwd_tile(const AttnParams& P, const Frag<D>& F, 
   // waves without a valid query (the tail block of S = 257) only help load
   if (wq0 < P.Sq && !(CAUSAL && kb > wq0 + 31)) {
     floatx16 sacc[2];
+    // the tile's second 32-key half is skipped (scores -inf, no MFMAs) when
+    // every key in it is past kv_len (the tail tile of S = 257) or above the
+    // causal diagonal of all this wave's queries (wave-uniform)
+    const bool half2 = P.full_tiles || (kb + 32 < kv_len && !(CAUSAL && kb + 32 > wq0 + 31));
     // all K fragments of the tile up front: the 16 LDS reads overlap each
     // other instead of one exposed LDS latency per MFMA
     short8 kfr[2][D / 16];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s) kfr[t][s] = F.row(kt, t, s);
+      for (int s = 0; s < D / 16; ++s)
+        if (t == 0 || half2) kfr[t][s] = F.row(kt, t, s);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
+      if (t == 1 && !half2) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[t][i] = -INFINITY;
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < 16; ++i) sacc[t][i] = 0.f;
 #pragma unroll
@@ -384,7 +395,8 @@ __device__ __forceinline__ void fwd_tile(const AttnParams& P, const Frag<D>& F, 
         }
     }
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < 2; ++t) {
+      if (t == 1 && !half2) continue;  // P = 0 there
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
         short8 pf;
@@ -394,6 +406,7 @@ __device__ __forceinline__ void fwd_tile(const AttnParams& P, const Frag<D>& F, 
         for (int dt = 0; dt < D / 32; ++dt)
           oacc[dt] = mfma<T>(F.tr(vt, t, ss, dt), pf, oacc[dt]);
       }
+    }
   }
 }
 
@@ -959,6 +972,8 @@ AttnParams make_params(const void* q, const void* k, const void* v, const long* 
   P.khi = (uint32_t)(key >> 32);
   P.thr = (uint32_t)(p * 65536.0f + 0.5f);
   P.drop_scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  static const int half_skip = [] { const char* e = getenv("FLEETX_FA_HALF_SKIP"); return e ? atoi(e) : 1; }();
+  P.full_tiles = !half_skip;
   P.salt = p > 0.f ? g_fx_dropout_salt : nullptr;
   return P;
 }
