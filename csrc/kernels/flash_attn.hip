@@ -238,6 +238,7 @@ struct AttnParams {
   int delta_in_dq;       // backward: the dQ pass computes and stores delta (no pre-pass)
   const uint64_t* salt;  // graph mode: per-replay device salt (fx_set_dropout_salt)
   int full_tiles;        // forward: compute fully masked key halves too (A/B, FLEETX_FA_HALF_SKIP=0)
+  int dq_half_skip;      // dQ: skip fully masked key halves (FLEETX_FA_DQ_HALF_SKIP=1)
 };
 
 // per-(batch, head) dropout hash seed; under graph mode the baked key is
@@ -644,8 +645,12 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
     // waves without a valid query (the tail block of S = 257) only help load
     if (wq0 < P.Sq && !(CAUSAL && kb > wq0 + 31)) {
       const bool need_mask = (CAUSAL && kb + KV - 1 > wq0) || (kb + KV > kv_len);
+      // second 32-key half fully masked (P = 0 there, so dS = 0): skipped as in
+      // the forward when FLEETX_FA_DQ_HALF_SKIP=1 (opt-in until measured)
+      const bool half2 = !P.dq_half_skip || (kb + 32 < kv_len && !(CAUSAL && kb + 32 > wq0 + 31));
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
+        if (t == 1 && !half2) continue;
         floatx16 sacc, dpacc;
 #pragma unroll
         for (int i = 0; i < 16; ++i) sacc[i] = dpacc[i] = 0.f;
@@ -974,6 +979,8 @@ AttnParams make_params(const void* q, const void* k, const void* v, const long* 
   P.drop_scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   static const int half_skip = [] { const char* e = getenv("FLEETX_FA_HALF_SKIP"); return e ? atoi(e) : 1; }();
   P.full_tiles = !half_skip;
+  static const int dq_skip = [] { const char* e = getenv("FLEETX_FA_DQ_HALF_SKIP"); return e ? atoi(e) : 0; }();
+  P.dq_half_skip = dq_skip;
   P.salt = p > 0.f ? g_fx_dropout_salt : nullptr;
   return P;
 }
