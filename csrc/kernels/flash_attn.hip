@@ -238,7 +238,7 @@ struct AttnParams {
   int delta_in_dq;       // backward: the dQ pass computes and stores delta (no pre-pass)
   const uint64_t* salt;  // graph mode: per-replay device salt (fx_set_dropout_salt)
   int full_tiles;        // forward: compute fully masked key halves too (A/B, FLEETX_FA_HALF_SKIP=0)
-  int dq_half_skip;      // dQ: skip fully masked key halves (FLEETX_FA_DQ_HALF_SKIP=1)
+  int dq_half_skip;      // dQ: skip fully masked key halves (FLEETX_FA_DQ_HALF_SKIP=0 turns it off)
 };
 
 // per-(batch, head) dropout hash seed; under graph mode the baked key is
@@ -646,7 +646,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
     if (wq0 < P.Sq && !(CAUSAL && kb > wq0 + 31)) {
       const bool need_mask = (CAUSAL && kb + KV - 1 > wq0) || (kb + KV > kv_len);
       // second 32-key half fully masked (P = 0 there, so dS = 0): skipped as in
-      // the forward when FLEETX_FA_DQ_HALF_SKIP=1 (opt-in until measured)
+      // the forward (ViT-g backward 291.8 -> 280.0 us, causal D 64 / 128
+      // neutral: profiles/r3_fahalf/; FLEETX_FA_DQ_HALF_SKIP=0 for A/B)
       const bool half2 = !P.dq_half_skip || (kb + 32 < kv_len && !(CAUSAL && kb + 32 > wq0 + 31));
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -979,7 +980,7 @@ AttnParams make_params(const void* q, const void* k, const void* v, const long* 
   P.drop_scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   static const int half_skip = [] { const char* e = getenv("FLEETX_FA_HALF_SKIP"); return e ? atoi(e) : 1; }();
   P.full_tiles = !half_skip;
-  static const int dq_skip = [] { const char* e = getenv("FLEETX_FA_DQ_HALF_SKIP"); return e ? atoi(e) : 0; }();
+  static const int dq_skip = [] { const char* e = getenv("FLEETX_FA_DQ_HALF_SKIP"); return e ? atoi(e) : 1; }();
   P.dq_half_skip = dq_skip;
   P.salt = p > 0.f ? g_fx_dropout_salt : nullptr;
   return P;
