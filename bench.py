@@ -33,8 +33,9 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 # Multi-rank: one HIP hardware queue per peer-waiting stream (compute + one per
 # RCCL communicator), set before the HIP runtime initialises
 # (fleetx_amd/utils/streams.py; the pool allows up to 32).
-if int(os.environ.get("WORLD_SIZE", "1")) > 1 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    from fleetx_amd.utils.streams import ensure_hw_queues  # noqa: E402
+    ensure_hw_queues(8)
 
 MODELS = {
     # name: (hidden, layers, heads)

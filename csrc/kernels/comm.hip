@@ -28,7 +28,9 @@
 //    checkpoint save or data stall does not trip it); a timeout never
 //    produces a normal-looking result: the affected outputs are written as
 //    NaN (so the loss / found-inf / NaN guard see it on the next step) and
-//    *err is set, which the engine reads at every logging sync and raises.
+//    *err is set, which the engine reads at every logging sync and raises;
+//    while *err is set later calls do not spin at all (they see it at entry),
+//    and the optimizer folds it into found_inf so the step is skipped.
 //    The protocol itself survives a timeout: the late peer still finds this
 //    rank's pushed granules of that call, and the next call uses the other
 //    parity, so only the timed-out call's output is lost.
@@ -100,9 +102,14 @@ template <typename T, int OP>  // OP 0 = sum, 1 = max
 __global__ __launch_bounds__(FX_COMM_THREADS) void ll_allreduce_kernel(
     const T* in, T* out, long n, int rank, int world, PeerTable pt, unsigned int* epochs,
     unsigned int* err, long slot, unsigned long long timeout) {
-  __shared__ unsigned int s_epoch;
+  __shared__ unsigned int s_epoch, s_err;
   const int b = blockIdx.x;
-  if (threadIdx.x == 0) s_epoch = epochs[b] + 1u;
+  if (threadIdx.x == 0) {
+    s_epoch = epochs[b] + 1u;
+    // a peer already timed out (dead or stalled): do not spin again -- every
+    // granule not yet present becomes NaN at once
+    s_err = __hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   __syncthreads();
   const unsigned int e = s_epoch;
   const int par = e & 1;
@@ -121,7 +128,7 @@ __global__ __launch_bounds__(FX_COMM_THREADS) void ll_allreduce_kernel(
   }
   // 2) reduce in rank order; poll every peer granule until its tag is ours
   const unsigned long long* mine = pt.recv[rank];
-  bool timed_out = false;
+  bool timed_out = s_err != 0u;
   for (long g = g0 + threadIdx.x; g < g1; g += blockDim.x) {
     float acc[2] = {0.f, 0.f};
     bool lost = false;

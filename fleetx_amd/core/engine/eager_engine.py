@@ -153,11 +153,13 @@ class EagerEngine(BasicEngine):
         self._metrics_file = e.get("metrics_file") or os.environ.get("FLEETX_METRICS_FILE")
         self._fault = os.environ.get("FLEETX_FAULT_INJECT")  # "rank:step" -> os._exit(17)
         # GEMM kinds on the MFMA kernel under FLEETX_GEMM=auto, per model
-        # (the env var FLEETX_GEMM_AUTO wins): e.g. ViT-g's data gradients
+        # (the env var FLEETX_GEMM_AUTO wins): e.g. ViT-g's data gradients.
+        # Always (re)set, so an engine without the key does not inherit the
+        # routing of an earlier engine in the same process.
+        from ...ops import gemm as _gemm
         routing = e.get("gemm_routing")
-        if routing and "FLEETX_GEMM_AUTO" not in os.environ:
-            from ...ops import gemm as _gemm
-            _gemm.set_auto_kinds(routing)
+        _gemm.set_auto_kinds(routing if routing and "FLEETX_GEMM_AUTO" not in os.environ
+                             else _gemm.default_auto_kinds())
 
         self.hcg = topo.get_hcg()
         self._dp_rank = self.hcg.dp_rank

@@ -125,8 +125,9 @@ def child_env(args, devices, local_rank, attempt, master_addr, master_port):
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     # one HIP hardware queue per peer-waiting stream for multi-rank jobs
     # (utils/streams.py): RCCL communicators must not share in-order queues
-    if world > 1 and int(env.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
-        env["GPU_MAX_HW_QUEUES"] = "8"
+    if world > 1:
+        from .utils.streams import ensure_hw_queues
+        ensure_hw_queues(8, env=env)
     return env
 
 

@@ -105,28 +105,7 @@ class GPTForPretrainingPipe(nn.Module):
         tokens, pos, labels, mask = self._split(data, m)
         mb, s = tokens[0].shape
         sched = self._schedule_for((mb, s, self.cfg.hidden_size))
-        if self.V > 1:
-            # evaluate chunk by chunk through the ring: reuse forward_only per chunk order
-            return self._eval_interleaved(sched, m, tokens, pos, labels, mask)
-        return sched.forward_only(m, self._stage_fn(m, tokens, pos, labels, mask))
-
-    def _eval_interleaved(self, sched, m, tokens, pos, labels, mask):
         fn = self._stage_fn(m, tokens, pos, labels, mask)
-        losses = []
-        p2p = sched.p2p
-        for k in range(m):
-            x = None
-            for c in range(self.V):
-                first_v = p2p.stage == 0 and c == 0
-                last_v = p2p.stage == p2p.nstages - 1 and c == self.V - 1
-                if not first_v:
-                    x = p2p.exchange(recv_prev=sched._buf())[0]
-                y = fn(c, k, x)
-                if last_v:
-                    losses.append(y)
-                else:
-                    p2p.post(send_next=y)
-        p2p.drain()
-        if self.is_last:
-            return torch.stack(losses).sum()
-        return None
+        if self.V > 1:
+            return sched.forward_only_interleaved(m, fn)
+        return sched.forward_only(m, fn)

@@ -66,7 +66,14 @@ def set_mode(mode):
 # hidden 1024-2048 models and ViT-g use); FLEETX_GEMM_AUTO="kind,kind"
 # replaces the set.
 _DEFAULT_AUTO = "wgrad"
-AUTO_KINDS = set(k for k in os.environ.get("FLEETX_GEMM_AUTO", _DEFAULT_AUTO).split(",") if k)
+
+
+def default_auto_kinds():
+    """The process default: ``FLEETX_GEMM_AUTO`` or the built-in table."""
+    return os.environ.get("FLEETX_GEMM_AUTO", _DEFAULT_AUTO)
+
+
+AUTO_KINDS = set(k for k in default_auto_kinds().split(",") if k)
 MIN_TILES = int(os.environ.get("FLEETX_GEMM_MIN_TILES", "192"))
 # weight gradients whose tiles underfill the chip run split along K
 # (gemm5.hip g5_split_plan), so they may take smaller shapes

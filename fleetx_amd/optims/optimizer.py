@@ -115,6 +115,10 @@ class FlatOptimizer:
                     dist_sq = dist_sq + sq
                 else:
                     rep_sq = rep_sq + sq
+        err = getattr(self, "_comm_err", None)
+        if err is not None:
+            self._comm_err = None
+            dist_sq = dist_sq + torch.where(err[0] != 0, float("inf"), 0.0)
         shard = self.buffer.shard_group if self.buffer.shard_stage >= 1 else None
         if shard is not None:
             pair = torch.stack([dist_sq, rep_sq])
@@ -128,12 +132,23 @@ class FlatOptimizer:
         return torch.sqrt(total)
 
     def _prepare_scale(self):
-        """Device-side clip coefficient x loss-scale unscale, and found-inf."""
+        """Device-side clip coefficient x loss-scale unscale, and found-inf.
+
+        A timed-out one-shot all-reduce (``parallel/comm.py``) counts as an
+        overflow: with a norm, +inf joins the local sum of squares before the
+        shard / mp / pp reductions, so every rank of the check group skips the
+        step together; without one, the local flag is the found-inf."""
+        from ..parallel import comm as _comm
+        err = _comm.error_flag()
         need_norm = self.grad_clip is not None or self.loss_scale is not None
         if not need_norm:
             self.gscale.fill_(1.0)
-            self.found_inf.zero_()
+            if err is None:
+                self.found_inf.zero_()
+            else:
+                self.found_inf.copy_((err != 0).to(torch.int32))
             return
+        self._comm_err = err
         norm = self.compute_grad_norm()
         inv_scale = 1.0 / self.loss_scale if self.loss_scale is not None else 1.0
         true_norm = norm * inv_scale

@@ -26,6 +26,7 @@ _OPS = ("all_reduce", "all_gather_into_tensor", "reduce_scatter_tensor", "broadc
 _DTYPES = [torch.float32, torch.float16, torch.bfloat16, torch.float64, torch.int32,
            torch.int64, torch.uint8, torch.int8, torch.bool]
 _state = {"enabled": False, "orig": {}, "mirror": {}, "seq": {}, "world": None}
+_P2P_LEN = 9
 
 
 class CollectiveMismatch(RuntimeError):
@@ -75,6 +76,52 @@ def _check(op, group, t, extra=0):
         rows = "\n".join("  rank %d: %s" % (r, _describe(o)) for r, o in zip(ranks, out))
         raise CollectiveMismatch("collective fingerprint mismatch on group {}:\n{}".format(
             ranks, rows))
+
+
+def enabled():
+    return _state["enabled"]
+
+
+def _p2p_fp(seq, t):
+    shape = list(t.shape)
+    dt = _DTYPES.index(t.dtype) if t.dtype in _DTYPES else -1
+    return torch.tensor([seq, dt, t.numel(), len(shape)] + (shape + [0, 0, 0, 0])[:4] + [0],
+                        dtype=torch.int64)
+
+
+def _p2p_describe(row):
+    dt = _DTYPES[int(row[1])] if 0 <= int(row[1]) < len(_DTYPES) else "?"
+    nd = int(row[3])
+    return "#%d %s %s" % (int(row[0]), str(dt).replace("torch.", ""),
+                          tuple(int(x) for x in row[4:4 + min(nd, 4)]))
+
+
+def check_p2p(group, ops):
+    """Fingerprint one grouped p2p call (``ops = [(kind, tensor, peer)]``,
+    peer a global rank) against the matching calls of its peers."""
+    mirror = _state["mirror"].get(group)
+    if mirror is None:
+        return
+    works, checks = [], []
+    for kind, t, peer in ops:
+        key = (mirror, peer, kind)
+        seq = _state["seq"].get(key, 0)
+        _state["seq"][key] = seq + 1
+        fp = _p2p_fp(seq, t)
+        if kind == "send":
+            works.append(dist.isend(fp, dst=peer, group=mirror))
+        else:
+            got = torch.empty(_P2P_LEN, dtype=torch.int64)
+            works.append(dist.irecv(got, src=peer, group=mirror))
+            checks.append((peer, fp, got))
+    for w in works:
+        w.wait()
+    for peer, want, got in checks:
+        if not torch.equal(want, got):
+            raise CollectiveMismatch(
+                "p2p fingerprint mismatch: rank {} expects to receive {} from rank {}, "
+                "which sent {}".format(dist.get_rank(), _p2p_describe(want), peer,
+                                       _p2p_describe(got)))
 
 
 def _op_extra(rop):

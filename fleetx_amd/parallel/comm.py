@@ -240,6 +240,20 @@ def check_all():
         c.check()
 
 
+def error_flag():
+    """Device int32 ``[1]``: non-zero once any one-shot call of this process
+    timed out (no host sync), or ``None`` when no one-shot path exists.  The
+    optimizer folds it into the step's found-inf so a step whose collectives
+    lost a peer is skipped instead of applied."""
+    flags = [c.oneshot.err for c in _COMMS.values() if c.oneshot is not None]
+    if not flags:
+        return None
+    out = flags[0]
+    for f in flags[1:]:
+        out = out + f
+    return out
+
+
 def reset():
     for c in _COMMS.values():
         if c.oneshot is not None:

@@ -129,7 +129,12 @@ def accumulate_wgrad(weight, dy2, x2, bias=None, notify=True):
         return _accumulate_wgrad(weight, dy2, x2, bias, notify)
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
-        _accumulate_wgrad(weight, dy2, x2, bias, notify=False, bias_notify=False)
+        r = _accumulate_wgrad(weight, dy2, x2, bias, notify=False, bias_notify=False,
+                              kernel_only=True)
+    if r is _DECLINED:
+        # the kernel declined after all (rc != 0): the vendor fallback runs on
+        # the main stream, never concurrently with another stream-K GEMM
+        return _accumulate_wgrad(weight, dy2, x2, bias, notify)
     dy2.record_stream(side)
     x2.record_stream(side)
     # readiness callbacks may launch collectives: those join the side stream
@@ -140,7 +145,13 @@ def accumulate_wgrad(weight, dy2, x2, bias=None, notify=True):
     return None
 
 
-def _accumulate_wgrad(weight, dy2, x2, bias=None, notify=True, bias_notify=True):
+_DECLINED = object()
+
+
+def _accumulate_wgrad(weight, dy2, x2, bias=None, notify=True, bias_notify=True,
+                      kernel_only=False):
+    """``kernel_only``: return ``_DECLINED`` (nothing written) instead of
+    running the hipBLASLt fallback when the MFMA kernel declines."""
     mg = weight.main_grad
     fresh = getattr(weight, "_fx_fresh", False)
     # gradient-norm partials from the epilogue (grad_buffer.enable_fused_norm):
@@ -157,6 +168,8 @@ def _accumulate_wgrad(weight, dy2, x2, bias=None, notify=True, bias_notify=True)
             done = G.linear_wgrad(dy2, x2, mg, not fresh)
     elif sq is not None:
         weight._fx_sq_ok = False
+    if not done and kernel_only:
+        return _DECLINED
     if done:
         db = None
         if bias is not None:

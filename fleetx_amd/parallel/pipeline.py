@@ -9,36 +9,50 @@ warm-up forwards, steady 1F1B, cool-down backwards; activations / grads of
 the loss (averaged over micro-batches) and the tied embedding grad is reduced
 between the first and last stage.
 
-MI355X design:
-* grouped ``batch_isend_irecv`` calls (``ncclGroupStart/End``) on one RCCL
-  communicator per pipe group by default -- an in-order stream that is
-  deadlock-free whatever hardware queue it lands in; with
-  ``Distributed.comm.pp_split_directions`` activations (stage s -> s+1, and
-  the ring edge of the interleaved schedule) and gradients (s+1 -> s) get a
-  communicator each, so a gradient never queues behind an activation (needs
-  ``GPU_MAX_HW_QUEUES`` >= the peer-waiting streams, ``utils/streams.py``);
-* nothing waits for a SEND: the compute stream only waits for a receive, and
-  only where the received tensor is consumed (``_Recv.wait``).  Posting the
-  receive of the next micro-batch's input together with the current send lets
-  the transfer run under the backward pass that follows.  (With NCCL/RCCL a
-  ``Work.wait`` is a stream-level wait, not a host block.)  Pending sends are
-  retired at the end of the step;
-* the split is deadlock-free by construction: per direction, the k-th send on
-  a link meets the k-th receive on the other side, and separating the
-  directions / deferring waits only REMOVES ordering edges from the original
-  single-stream schedule;
+MI355X / RCCL design:
+* every exchange is ONE grouped ``batch_isend_irecv`` (``ncclGroupStart/End``)
+  on the pipe communicator.  RCCL runs the groups of one communicator in
+  order on one stream and a group finishes only when all of its sends and
+  receives have met their peers, so the posting order is what decides
+  whether a schedule can deadlock.  The schedules therefore post
+  MIRROR-IMAGE groups on both ends of every link, in the same order:
+  ``{send y_k -> s+1, recv dy_j <- s+1}`` on stage s meets
+  ``{send dx_j -> s, recv x_k+1 <- s}`` on stage s+1 (the steady-state
+  pairing of Megatron-LM's 1F1B).  ``tests/test_pipeline_order_cpu.py``
+  replays the posted groups of every schedule (1F1B, interleaved, forward-only,
+  interleaved forward-only; P up to 8) against an in-order-per-communicator
+  matcher (``parallel/p2p_replay.py``) and against host-blocking matching;
+* with ``Distributed.comm.pp_split_directions`` activations and gradients
+  get a communicator each (two groups per exchange); the same replay covers
+  that mode;
+* nothing waits for a SEND: the compute stream waits for a receive only where
+  the received tensor is consumed (``_Recv.wait``; with RCCL a ``Work.wait``
+  is a stream-level wait, not a host block).  Pending sends are retired at the
+  end of the step;
 * shapes are static (``[micro_b, s, h]`` in the model dtype), so there is no
-  per-step shape handshake;
+  per-step shape handshake; ``Distributed.debug: fingerprint`` checks them
+  (and the per-link order) pairwise over gloo (``collective_check.check_p2p``);
 * gradient-bucket reductions of the flat grad buffer are armed only for the
   LAST backward of the step and overlap the cool-down phase.
 """
 import torch
 import torch.distributed as dist
 
+from . import collective_check
+
+
+def issue_dist(group, ops):
+    """Issue ``ops`` (``[(kind, tensor, peer)]``, kind ``"send"``/``"recv"``,
+    peer a global rank) as one grouped call; returns the ``Work`` list (one
+    per op on gloo, one for the whole group on RCCL)."""
+    return dist.batch_isend_irecv([dist.P2POp(dist.isend if k == "send" else dist.irecv,
+                                              t, peer, group) for k, t, peer in ops])
+
 
 class _Recv:
     """A posted receive: ``wait()`` orders the consumer after the transfer and
-    returns the buffer."""
+    returns the buffer.  Receives of one coalesced group share the ``works``
+    list, which is emptied by the first wait (never wait a Work twice)."""
 
     __slots__ = ("buf", "works")
 
@@ -48,12 +62,12 @@ class _Recv:
     def wait(self):
         for w in self.works:
             w.wait()
-        self.works = ()
+        self.works.clear()
         return self.buf
 
 
 class P2P:
-    def __init__(self, hcg):
+    def __init__(self, hcg, issue=None):
         self.hcg = hcg
         g = hcg.get_pipe_parallel_group()
         gb = hcg.get_pipe_bwd_group() if hasattr(hcg, "get_pipe_bwd_group") else g
@@ -62,7 +76,8 @@ class P2P:
         self.ranks = g.ranks if g is not None else [0]
         self.stage = hcg.pp_rank
         self.nstages = hcg.pp_degree
-        self._warm = False
+        self.issue = issue or issue_dist
+        self._warm = issue is not None
         self._sends = []
 
     def warmup(self, device):
@@ -79,31 +94,55 @@ class P2P:
     def _peer(self, delta):
         return self.ranks[(self.stage + delta) % self.nstages]
 
-    def _post(self, group, send, send_peer, recv, recv_peer):
-        ops = []
-        if send is not None:
-            ops.append(dist.P2POp(dist.isend, send.contiguous(), send_peer, group))
-        if recv is not None:
-            ops.append(dist.P2POp(dist.irecv, recv, recv_peer, group))
-        if not ops:
-            return None
-        works = dist.batch_isend_irecv(ops)
-        if recv is None:
+    def _issue(self, group, ops):
+        """One grouped call; returns ``{recv buffer id: _Recv}``."""
+        if collective_check.enabled():
+            collective_check.check_p2p(group, ops)
+        works = list(self.issue(group, ops))
+        handles = {}
+        if len(works) == len(ops):          # one Work per op (gloo)
+            for (kind, t, _), w in zip(ops, works):
+                if kind == "recv":
+                    handles[id(t)] = _Recv(t, [w])
+                else:
+                    self._sends.append(w)
+            return handles
+        # one Work for the whole group (coalesced RCCL): the receives' wait
+        # covers the sends as well
+        recvs = [t for kind, t, _ in ops if kind == "recv"]
+        if not recvs:
             self._sends.extend(works)
-            return None
-        if len(works) == len(ops):       # one Work per op (gloo): split them
-            self._sends.extend(works[:-1])
-            return _Recv(recv, works[-1:])
-        # one Work for the whole group (coalesced RCCL/NCCL): the receive's
-        # wait covers the send as well -- never wait a Work twice (gloo hangs)
-        return _Recv(recv, works)
+        for t in recvs:
+            handles[id(t)] = _Recv(t, works)
+        return handles
 
     def post(self, send_next=None, send_prev=None, recv_prev=None, recv_next=None):
-        """Post a forward-direction group (send_next / recv_prev) and a
-        backward-direction group (send_prev / recv_next); returns
-        ``(recv_prev_handle, recv_next_handle)`` (``None`` where not asked)."""
-        hp = self._post(self.group, send_next, self._peer(1), recv_prev, self._peer(-1))
-        hn = self._post(self.group_bwd, send_prev, self._peer(-1), recv_next, self._peer(1))
+        """Post one exchange with the neighbouring stages; returns
+        ``(recv_prev_handle, recv_next_handle)`` (``None`` where not asked).
+
+        One communicator: all ops form ONE group.  Split directions: the
+        activation-direction ops (send_next / recv_prev) and the
+        gradient-direction ops (send_prev / recv_next) form one group each on
+        their own communicator."""
+        fwd, bwd = [], []
+        if send_next is not None:
+            fwd.append(("send", send_next.contiguous(), self._peer(1)))
+        if recv_prev is not None:
+            fwd.append(("recv", recv_prev, self._peer(-1)))
+        if send_prev is not None:
+            bwd.append(("send", send_prev.contiguous(), self._peer(-1)))
+        if recv_next is not None:
+            bwd.append(("recv", recv_next, self._peer(1)))
+        if self.group_bwd is self.group:
+            groups = [(self.group, fwd + bwd)]
+        else:
+            groups = [(self.group, fwd), (self.group_bwd, bwd)]
+        handles = {}
+        for g, ops in groups:
+            if ops:
+                handles.update(self._issue(g, ops))
+        hp = handles.get(id(recv_prev)) if recv_prev is not None else None
+        hn = handles.get(id(recv_next)) if recv_next is not None else None
         return hp, hn
 
     def exchange(self, send_next=None, send_prev=None, recv_prev=None, recv_next=None):
@@ -124,10 +163,11 @@ class PipelineSchedule:
     ``stage_fn(chunk, micro_idx, x)`` runs model chunk ``chunk`` on micro-batch
     ``micro_idx`` (``x`` is the received activation or None on the first
     stage) and returns the activation, or the scaled loss on the last stage.
+    ``p2p`` injects a transport (the order replay of ``p2p_replay.py``).
     """
 
-    def __init__(self, hcg, act_shape_fn, dtype, device, num_chunks=1):
-        self.p2p = P2P(hcg)
+    def __init__(self, hcg, act_shape_fn, dtype, device, num_chunks=1, p2p=None):
+        self.p2p = p2p if p2p is not None else P2P(hcg)
         self.hcg = hcg
         self.act_shape_fn = act_shape_fn
         self.dtype, self.device = dtype, device
@@ -139,40 +179,28 @@ class PipelineSchedule:
 
     # ------------------------------------------------------------------ 1F1B
     def train_1f1b(self, m, stage_fn, on_last_backward=None):
-        """Warm-up forwards, steady 1F1B, cool-down backwards.  The receive of
-        the next forward input rides with the current activation send, and the
-        receive of the next output gradient with the current input-gradient
-        send, so both transfers run under the compute that follows; the
-        compute stream waits for a receive only when it consumes it."""
+        """Warm-up forwards, steady 1F1B, cool-down backwards (stage s runs
+        ``min(P - s - 1, m)`` warm-up forwards).
+
+        Posting order (mirror image on the two ends of every link):
+        * warm-up: ``{recv x_i}``, forward, ``{send y_i}``;
+        * before the steady phase: ``{recv x_w}``;
+        * steady: forward k, ``{send y_k, recv dy_j}``, backward j,
+          ``{send dx_j, recv x_k+1}`` (the last one is ``{send dx_j}``);
+        * cool-down: ``{recv dy_j}``, backward j, ``{send dx_j}``.
+        The compute stream waits for a receive only where it consumes it."""
         p2p = self.p2p
         first, last = p2p.stage == 0, p2p.stage == p2p.nstages - 1
         warmup = min(p2p.nstages - p2p.stage - 1, m)
         remaining = m - warmup
         ins, outs, losses = [], [], []
         n_bwd = [0]
-        x_q, dy_q = [], []          # posted receives (forward inputs / output grads)
-        n_x, n_dy = [0], [0]        # receives posted so far
 
-        def want_x():
-            return not first and n_x[0] < m
+        def recv_x():
+            return None if first else p2p.post(recv_prev=self._buf())[0]
 
-        def want_dy():
-            return not last and n_dy[0] < m
-
-        def post(send_next=None, send_prev=None, rx=False, rdy=False):
-            bp = self._buf() if rx and want_x() else None
-            bn = self._buf() if rdy and want_dy() else None
-            hp, hn = p2p.post(send_next=send_next, send_prev=send_prev, recv_prev=bp,
-                              recv_next=bn)
-            if hp is not None:
-                x_q.append(hp)
-                n_x[0] += 1
-            if hn is not None:
-                dy_q.append(hn)
-                n_dy[0] += 1
-
-        def fwd(k):
-            x = x_q.pop(0).wait() if not first else None
+        def fwd(k, hx):
+            x = hx.wait() if hx is not None else None
             if x is not None:
                 x.requires_grad_(True)
             y = stage_fn(0, k, x)
@@ -182,7 +210,7 @@ class PipelineSchedule:
             outs.append(y)
             return y
 
-        def bwd():
+        def bwd(hdy):
             n_bwd[0] += 1
             if n_bwd[0] == m and on_last_backward is not None:
                 on_last_backward()
@@ -190,26 +218,30 @@ class PipelineSchedule:
             if last:
                 y.backward()
             else:
-                torch.autograd.backward(y, dy_q.pop(0).wait())
+                torch.autograd.backward(y, hdy.wait())
             return x.grad if x is not None else None
 
-        post(rx=True)                                   # input of micro-batch 0
-        for k in range(warmup):
-            y = fwd(k)
-            post(send_next=None if last else y.detach(), rx=True,
-                 rdy=(k == warmup - 1))                 # first output grad
-        if warmup == 0:
-            post(rdy=True)
-        for k in range(remaining):
-            y = fwd(warmup + k)
-            post(send_next=None if last else y.detach(), rx=True)
-            dx = bwd()
-            post(send_prev=None if first else dx, rdy=True)
-        for k in range(warmup):
-            dx = bwd()
-            post(send_prev=None if first else dx, rdy=True)
+        for i in range(warmup):                 # never on the last stage
+            y = fwd(i, recv_x())
+            p2p.post(send_next=y.detach())
+        hx = recv_x() if remaining > 0 else None
+        for i in range(remaining):
+            y = fwd(warmup + i, hx)
+            hdy = None if last else p2p.post(send_next=y.detach(), recv_next=self._buf())[1]
+            dx = bwd(hdy)
+            if i == remaining - 1:
+                hx = None
+                if not first:
+                    p2p.post(send_prev=dx)
+            elif not first:
+                hx = p2p.post(send_prev=dx, recv_prev=self._buf())[0]
+        for i in range(warmup):
+            hdy = p2p.post(recv_next=self._buf())[1]
+            dx = bwd(hdy)
+            if not first:
+                p2p.post(send_prev=dx)
         p2p.drain()
-        assert not x_q and not dy_q, "pipeline receive queue not drained"
+        assert not ins and not outs, "pipeline activations not consumed"
         if last:
             return torch.stack(losses).sum()
         return None
@@ -223,11 +255,12 @@ class PipelineSchedule:
         ``(u // P) % V`` on micro-batch ``(u // (P V)) P + u % P`` in forward,
         and the mirrored chunk in backward; the warm-up is
         ``2 (P - rank - 1) + (V - 1) P`` units.  Every p2p step posts the sends
-        of this rank together with the receives it needs next (one grouped call
-        per direction), and the k-th send on a link always meets the k-th
-        receive on the other side (the chunk shift on the ring edge is a +P
-        unit shift, which preserves order), so the schedule cannot deadlock;
-        receives are waited for where consumed.  Requires ``m % P == 0``.
+        of this rank together with the receives it needs next as ONE group
+        (Megatron-LM's ``send_forward_backward_recv_forward_backward``); each
+        rank posts the same number of exchanges and the k-th send on a link
+        meets the k-th receive on the other side (the chunk shift on the ring
+        edge is a +P unit shift, which preserves order).  Receives are waited
+        for where consumed.  Requires ``m % P == 0``.
         """
         p2p = self.p2p
         P, V, r = p2p.nstages, self.num_chunks, p2p.stage
@@ -341,5 +374,26 @@ class PipelineSchedule:
                 p2p.post(send_next=y)
         p2p.drain()
         if last:
+            return torch.stack(losses).sum()
+        return None
+
+    @torch.no_grad()
+    def forward_only_interleaved(self, m, stage_fn):
+        """Evaluation through the virtual-stage ring: micro-batch by
+        micro-batch, chunk by chunk (``{recv x}``, forward, ``{send y}``)."""
+        p2p = self.p2p
+        P, V, r = p2p.nstages, self.num_chunks, p2p.stage
+        losses = []
+        for k in range(m):
+            for c in range(V):
+                first_v, last_v = r == 0 and c == 0, r == P - 1 and c == V - 1
+                x = None if first_v else p2p.exchange(recv_prev=self._buf())[0]
+                y = stage_fn(c, k, x)
+                if last_v:
+                    losses.append(y.detach())
+                else:
+                    p2p.post(send_next=y)
+        p2p.drain()
+        if r == P - 1:
             return torch.stack(losses).sum()
         return None

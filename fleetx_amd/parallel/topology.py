@@ -23,6 +23,66 @@ import torch.distributed as dist
 
 _HCG = None
 
+# Per-communicator RCCL CTA budget (``Distributed.comm.ctas.<key>``): every
+# RCCL channel is one workgroup resident on a CU for the whole collective, so
+# the budget is set per group by what the group overlaps with, not by one
+# process-wide NCCL_MIN_NCHANNELS:
+#  * mp (TP all-reduce / SP gather-scatter): on the critical path, nothing to
+#    share the CUs with -> many channels;
+#  * dp / sharding / data_world (gradient buckets, ZeRO gathers): overlapped
+#    with backward GEMMs that want all 256 CUs -> capped;
+#  * pp (activation p2p) and the tied-embedding pair: medium;
+#  * check (norm / found-inf scalars): latency-bound -> few.
+# ``(min_ctas, max_ctas)``; ``None`` leaves the bound to RCCL.
+CTA_KEYS = {"dp": "data", "mp": "model", "pp": "pipe", "sharding": "sharding",
+            "data_world": "data_world", "check": "check", "embedding": "embedding"}
+DEFAULT_CTAS = {"model": (32, 64), "data": (8, 16), "sharding": (8, 16),
+                "data_world": (8, 16), "pipe": (4, 16), "check": (1, 4),
+                "embedding": (8, 32)}
+
+
+def parse_ctas(cfg):
+    """``Distributed.comm.ctas`` -> ``{group name: (min, max)}`` over the
+    defaults.  Values: ``"min,max"``, ``[min, max]`` or an int (max only);
+    ``None`` / ``False`` for a key drops the bound; ``ctas: False`` drops all."""
+    if cfg is False:
+        return {}
+    out = dict(DEFAULT_CTAS)
+    for k, v in dict(cfg or {}).items():
+        name = CTA_KEYS.get(k, k)
+        if name not in DEFAULT_CTAS:
+            raise ValueError("Distributed.comm.ctas: unknown group %r (keys: %s)"
+                             % (k, ", ".join(sorted(CTA_KEYS))))
+        if v in (None, False):
+            out.pop(name, None)
+            continue
+        if isinstance(v, str):
+            v = [int(x) for x in v.split(",")]
+            v = v[0] if len(v) == 1 else v
+        if isinstance(v, int):
+            v = (None, v)
+        lo, hi = v
+        if lo is not None and hi is not None and lo > hi:
+            raise ValueError("Distributed.comm.ctas.%s: min %d > max %d" % (k, lo, hi))
+        out[name] = (lo, hi)
+    out["pipe_bwd"] = out.get("pipe")
+    if out["pipe_bwd"] is None:
+        out.pop("pipe_bwd")
+    return out
+
+
+def nccl_options(ctas):
+    """``ProcessGroupNCCL.Options`` carrying ``(min_ctas, max_ctas)``."""
+    if ctas is None:
+        return None
+    opts = dist.ProcessGroupNCCL.Options()
+    lo, hi = ctas
+    if lo is not None:
+        opts.config.min_ctas = int(lo)
+    if hi is not None:
+        opts.config.max_ctas = int(hi)
+    return opts
+
 
 class ParallelMode:
     DATA_PARALLEL = 0
@@ -89,7 +149,7 @@ class HybridTopology:
 class HybridCommunicateGroup:
     """Holds every communicator of the hybrid layout for this rank."""
 
-    def __init__(self, dp=1, mp=1, pp=1, sharding=1, pp_split_directions=False):
+    def __init__(self, dp=1, mp=1, pp=1, sharding=1, pp_split_directions=False, ctas=None):
         self.topo = HybridTopology(dp=dp, pp=pp, sharding=sharding, mp=mp)
         self.initialized = dist.is_initialized()
         self.global_rank = dist.get_rank() if self.initialized else 0
@@ -100,16 +160,18 @@ class HybridCommunicateGroup:
         coord = self.topo.get_coord(self.global_rank)
         self.dp_rank, self.pp_rank, self.sharding_rank, self.mp_rank = coord
         self.stage_id = self.pp_rank
+        self._nccl = self.initialized and dist.get_backend() == "nccl"
+        self.ctas = parse_ctas(ctas) if ctas is not False else {}
 
         self._groups = {}
         for axis in HybridTopology.AXES:
-            self._groups[axis] = self._build(self.topo.axis_groups(axis))
+            self._groups[axis] = self._build(self.topo.axis_groups(axis), axis)
         # data world = dp x sharding (reference env.py:76-96)
-        self._groups["data_world"] = self._build(self._data_world_groups())
+        self._groups["data_world"] = self._build(self._data_world_groups(), "data_world")
         # "check" group: mp x pp x sharding for global-norm / found-inf reductions
-        self._groups["check"] = self._build(self._check_groups())
+        self._groups["check"] = self._build(self._check_groups(), "check")
         # first/last pipeline stage pairs for the tied embedding
-        self._groups["embedding"] = self._build(self._embedding_groups())
+        self._groups["embedding"] = self._build(self._embedding_groups(), "embedding")
         # Optional second communicator over each pipe group
         # (Distributed.comm.pp_split_directions): backward-direction p2p gets
         # its own RCCL stream.  Off by default: with more peer-waiting streams
@@ -117,14 +179,20 @@ class HybridCommunicateGroup:
         # hardware queue in opposite orders on neighbouring stages
         # (utils/streams.py); one communicator is deadlock-free whatever the
         # mapping.
-        self._groups["pipe_bwd"] = self._build(self.topo.axis_groups("pipe")) \
+        self._groups["pipe_bwd"] = self._build(self.topo.axis_groups("pipe"), "pipe_bwd") \
             if pp > 1 and pp_split_directions else self._groups["pipe"]
 
-    def _build(self, rank_lists):
+    def pg_options(self, name):
+        """RCCL options of group ``name`` (None on gloo or without a budget)."""
+        return nccl_options(self.ctas.get(name)) if self._nccl else None
+
+    def _build(self, rank_lists, name):
         mine = None
+        opts = self.pg_options(name)
         for ranks in rank_lists:
             if self.initialized and len(ranks) > 1:
-                g = dist.new_group(ranks=ranks)
+                g = dist.new_group(ranks=ranks, pg_options=opts) if opts is not None \
+                    else dist.new_group(ranks=ranks)
                 gg = dist.new_group(ranks=ranks, backend="gloo") if _want_gloo() else None
             else:
                 g, gg = None, None
@@ -235,10 +303,10 @@ def _want_gloo():
     return os.environ.get("FLEETX_GLOO_SIDE_GROUPS", "0") == "1"
 
 
-def init_hcg(dp=1, mp=1, pp=1, sharding=1, pp_split_directions=False):
+def init_hcg(dp=1, mp=1, pp=1, sharding=1, pp_split_directions=False, ctas=None):
     global _HCG
     _HCG = HybridCommunicateGroup(dp=dp, mp=mp, pp=pp, sharding=sharding,
-                                  pp_split_directions=pp_split_directions)
+                                  pp_split_directions=pp_split_directions, ctas=ctas)
     return _HCG
 
 
@@ -259,6 +327,66 @@ def set_hcg(hcg):
 def reset_hcg():
     global _HCG
     _HCG = None
+
+# Per-communicator RCCL CTA budget (``Distributed.comm.ctas.<key>``): every
+# RCCL channel is one workgroup resident on a CU for the whole collective, so
+# the budget is set per group by what the group overlaps with, not by one
+# process-wide NCCL_MIN_NCHANNELS:
+#  * mp (TP all-reduce / SP gather-scatter): on the critical path, nothing to
+#    share the CUs with -> many channels;
+#  * dp / sharding / data_world (gradient buckets, ZeRO gathers): overlapped
+#    with backward GEMMs that want all 256 CUs -> capped;
+#  * pp (activation p2p) and the tied-embedding pair: medium;
+#  * check (norm / found-inf scalars): latency-bound -> few.
+# ``(min_ctas, max_ctas)``; ``None`` leaves the bound to RCCL.
+CTA_KEYS = {"dp": "data", "mp": "model", "pp": "pipe", "sharding": "sharding",
+            "data_world": "data_world", "check": "check", "embedding": "embedding"}
+DEFAULT_CTAS = {"model": (32, 64), "data": (8, 16), "sharding": (8, 16),
+                "data_world": (8, 16), "pipe": (4, 16), "check": (1, 4),
+                "embedding": (8, 32)}
+
+
+def parse_ctas(cfg):
+    """``Distributed.comm.ctas`` -> ``{group name: (min, max)}`` over the
+    defaults.  Values: ``"min,max"``, ``[min, max]`` or an int (max only);
+    ``None`` / ``False`` for a key drops the bound; ``ctas: False`` drops all."""
+    if cfg is False:
+        return {}
+    out = dict(DEFAULT_CTAS)
+    for k, v in dict(cfg or {}).items():
+        name = CTA_KEYS.get(k, k)
+        if name not in DEFAULT_CTAS:
+            raise ValueError("Distributed.comm.ctas: unknown group %r (keys: %s)"
+                             % (k, ", ".join(sorted(CTA_KEYS))))
+        if v in (None, False):
+            out.pop(name, None)
+            continue
+        if isinstance(v, str):
+            v = [int(x) for x in v.split(",")]
+            v = v[0] if len(v) == 1 else v
+        if isinstance(v, int):
+            v = (None, v)
+        lo, hi = v
+        if lo is not None and hi is not None and lo > hi:
+            raise ValueError("Distributed.comm.ctas.%s: min %d > max %d" % (k, lo, hi))
+        out[name] = (lo, hi)
+    out["pipe_bwd"] = out.get("pipe")
+    if out["pipe_bwd"] is None:
+        out.pop("pipe_bwd")
+    return out
+
+
+def nccl_options(ctas):
+    """``ProcessGroupNCCL.Options`` carrying ``(min_ctas, max_ctas)``."""
+    if ctas is None:
+        return None
+    opts = dist.ProcessGroupNCCL.Options()
+    lo, hi = ctas
+    if lo is not None:
+        opts.config.min_ctas = int(lo)
+    if hi is not None:
+        opts.config.max_ctas = int(hi)
+    return opts
     from . import comm
     comm.reset()
 

@@ -25,14 +25,14 @@ def get_world_size():
     return int(os.environ.get("WORLD_SIZE", "1"))
 
 
-# RCCL settings for the large data-parallel / ZeRO gradient buckets and
-# parameter all-gathers (Distributed.comm.rccl_env overrides; the process
-# environment always wins).  An 8-GPU MI355X node is a fully connected xGMI
-# mesh (7 point-to-point links per GPU): a bandwidth-optimal collective needs
-# enough channels that every link carries one, so the channel floor is
-# raised to 32 (RCCL picks fewer for some sizes).  tools/bench_collectives.py
-# reports bus bandwidth against the per-link rate.
-DEFAULT_RCCL_ENV = {"NCCL_MIN_NCHANNELS": "32"}
+# Process-wide RCCL environment (Distributed.comm.rccl_env; the process
+# environment always wins).  Empty by default: the channel (CTA) budget is
+# set PER COMMUNICATOR from Distributed.comm.ctas (parallel/topology.py
+# DEFAULT_CTAS) -- TP groups get many channels, gradient-bucket groups that
+# overlap backward GEMMs a capped number, scalar groups few -- instead of one
+# NCCL_MIN_NCHANNELS for every group.  tools/bench_collectives.py takes the
+# same keys.
+DEFAULT_RCCL_ENV = {}
 
 
 def apply_rccl_env(config=None):
@@ -71,7 +71,8 @@ def init_dist_env(config, backend=None):
     comm = d.get("comm", {}) or {}
     hcg = topo.init_hcg(dp=d.dp_degree, mp=d.mp_degree, pp=d.pp_degree,
                         sharding=d.sharding.sharding_degree,
-                        pp_split_directions=bool(comm.get("pp_split_directions", False)))
+                        pp_split_directions=bool(comm.get("pp_split_directions", False)),
+                        ctas=comm.get("ctas", None))
     if dbg == "fingerprint":
         # per-collective op / sequence / shape / dtype cross-check over gloo
         # mirrors of every group (parallel/collective_check.py)

@@ -44,20 +44,23 @@ def side_stream(device):
     return s
 
 
-def hw_queues():
+def hw_queues(env=None):
+    env = os.environ if env is None else env
     try:
-        return int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+        return int(env.get("GPU_MAX_HW_QUEUES", "4") or 4)
     except ValueError:
         return 4
 
 
-def ensure_hw_queues(n=8, limit=32):
-    """Raise ``GPU_MAX_HW_QUEUES`` to ``n`` (never lower it, never above
-    ``limit``).  Only effective before the HIP runtime initialises."""
-    cur = hw_queues()
+def ensure_hw_queues(n=8, limit=32, env=None):
+    """Raise ``GPU_MAX_HW_QUEUES`` in ``env`` (default: this process) to ``n``
+    (never lower it, never above ``limit``).  Only effective before the HIP
+    runtime of that process initialises."""
+    env = os.environ if env is None else env
+    cur = hw_queues(env)
     want = min(max(cur, n), limit)
-    if want != cur or "GPU_MAX_HW_QUEUES" not in os.environ:
-        os.environ["GPU_MAX_HW_QUEUES"] = str(want)
+    if want != cur or "GPU_MAX_HW_QUEUES" not in env:
+        env["GPU_MAX_HW_QUEUES"] = str(want)
     return want
 
 
@@ -81,7 +84,9 @@ def inventory(hcg=None, optimizer=None, buffer=None, wgrad_stream=False):
             if g is None or g.group is None or id(g.group) in seen:
                 continue
             seen.add(id(g.group))
-            out.append(("rccl:%s%s" % (name, list(g.ranks)), True))
+            c = getattr(hcg, "ctas", {}).get(name) if getattr(hcg, "_nccl", False) else None
+            budget = "" if c is None else "(ctas %s-%s)" % (c[0] or "auto", c[1] or "auto")
+            out.append(("rccl:%s%s%s" % (name, list(g.ranks), budget), True))
     return out
 
 

@@ -1,0 +1,65 @@
+"""Per-communicator RCCL CTA budget (``Distributed.comm.ctas``): parsing, and
+that the options reach ``new_group`` for every group of the hybrid topology.
+
+Reference collective call sites the groups serve: ``eager_engine.py:386-396``
+(DP/sharding reductions), ``tensor_fusion_helper.py:119-127`` (fused buckets),
+``sequence_parallel_utils.py:55,69,139`` (TP/SP).
+"""
+import pytest
+
+from fleetx_amd.parallel import topology as topo
+from tests import dist_utils
+
+
+def test_parse_defaults_and_overrides():
+    d = topo.parse_ctas(None)
+    assert d["model"] == (32, 64) and d["data"] == (8, 16) and d["check"] == (1, 4)
+    assert d["pipe_bwd"] == d["pipe"]
+    o = topo.parse_ctas({"dp": "4,8", "mp": 48, "pp": [2, 4], "check": None})
+    assert o["data"] == (4, 8) and o["model"] == (None, 48) and o["pipe"] == (2, 4)
+    assert "check" not in o and o["pipe_bwd"] == (2, 4)
+    assert topo.parse_ctas(False) == {}
+    with pytest.raises(ValueError):
+        topo.parse_ctas({"bogus": 4})
+    with pytest.raises(ValueError):
+        topo.parse_ctas({"dp": "16,8"})
+
+
+def test_nccl_options_carry_budget():
+    o = topo.nccl_options((8, 16))
+    assert o.config.min_ctas == 8 and o.config.max_ctas == 16
+    assert topo.nccl_options(None) is None
+
+
+def _build(rank, world, ctas):
+    import torch.distributed as dist
+    seen = []
+    real = dist.new_group
+
+    def fake_new_group(ranks=None, pg_options=None, **kw):
+        if pg_options is not None:
+            seen.append((tuple(ranks), pg_options.config.min_ctas, pg_options.config.max_ctas))
+        elif kw.get("backend") is None:
+            seen.append((tuple(ranks), None, None))
+        return real(ranks=ranks, **kw)
+
+    topo.dist.new_group = fake_new_group
+    topo.dist.get_backend = lambda *a, **k: "nccl"     # pretend RCCL for the options path
+    topo.reset_hcg()
+    hcg = topo.init_hcg(dp=2, mp=2, pp=2, ctas=ctas)
+    from fleetx_amd.utils.streams import inventory
+    names = [n for n, _ in inventory(hcg)]
+    return {"seen": seen, "inv": names}
+
+
+def test_options_reach_new_group():
+    res = dist_utils.run(_build, 8, {"dp": "4,12"})
+    seen = res[0]["seen"]
+    # the axis groups are built in order data, pipe, sharding(1: none), model
+    by = {}
+    for ranks, lo, hi in seen:
+        by.setdefault((lo, hi), []).append(ranks)
+    assert (4, 12) in by and (0, 4) in by[(4, 12)]          # dp groups: ranks differ by 4
+    assert (32, 64) in by and (0, 1) in by[(32, 64)]        # mp groups: adjacent ranks
+    assert (4, 16) in by and (0, 2) in by[(4, 16)]          # pp groups
+    assert any("rccl:model[0, 1](ctas 32-64)" == n for n in res[0]["inv"])

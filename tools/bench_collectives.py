@@ -19,9 +19,13 @@ JSON line per (op, size) from rank 0:
 
 The framework's large-message traffic is the data-parallel / ZeRO gradient
 buckets (``Distributed.comm.dp_bucket_mb``, 256 MiB by default) and the ZeRO
-parameter all-gather; ``Distributed.comm.rccl_env`` (utils/env.py) sets the
-RCCL channel count for them.  Numbers are only meaningful on a multi-GPU node
-(RCCL refuses two ranks on one device).
+parameter all-gather.  The communicator's CTA (channel) budget takes the same
+keys as ``Distributed.comm.ctas`` (``parallel/topology.py``): ``--ctas dp``
+benchmarks with the data-parallel group's default ``(min, max)``,
+``--ctas 8,16`` with an explicit one, ``--ctas none`` with RCCL's own choice,
+so the first 8-GPU run can A/B them; ``--rccl-env K=V,...`` exports extra RCCL
+variables.  Numbers are only meaningful on a multi-GPU node (RCCL refuses two
+ranks on one device).
 """
 import argparse
 import json
@@ -38,6 +42,17 @@ BUS_FACTOR = {
 }
 
 
+def cta_budget(spec):
+    """``--ctas`` -> ``(min, max)`` or None (same keys / value forms as
+    ``Distributed.comm.ctas``)."""
+    from fleetx_amd.parallel import topology as topo
+    if spec in (None, "", "none"):
+        return None
+    if spec in topo.CTA_KEYS:
+        return topo.parse_ctas(None).get(topo.CTA_KEYS[spec])
+    return topo.parse_ctas({"dp": spec})["data"]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--min-mb", type=float, default=1)
@@ -46,16 +61,28 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--ops", default="all_reduce,reduce_scatter,all_gather,all_to_all")
     ap.add_argument("--link-GBps", type=float, default=153.0)
+    ap.add_argument("--ctas", default="none",
+                    help="CTA budget of the benchmarked communicator: a Distributed.comm.ctas "
+                         "key (dp, mp, pp, sharding, data_world, check, embedding), 'min,max', "
+                         "or 'none'")
+    ap.add_argument("--rccl-env", default="", help="extra RCCL env, K=V[,K=V]")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
-    from fleetx_amd.utils.env import apply_rccl_env
+    from fleetx_amd.parallel import topology as topo
 
-    apply_rccl_env(None)
+    for kv in (x for x in args.rccl_env.split(",") if x):
+        k, v = kv.split("=", 1)
+        os.environ.setdefault(k, v)
+    budget = cta_budget(args.ctas)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    # the benchmarked communicator: the whole world with the chosen budget
+    opts = topo.nccl_options(budget)
+    grp = dist.new_group(ranks=list(range(dist.get_world_size())), pg_options=opts) \
+        if opts is not None else None
     n = dist.get_world_size()
     rank = dist.get_rank()
     dt = torch.bfloat16
@@ -70,16 +97,16 @@ def main():
             numel = nbytes // esz // n * n
             x = torch.randn(numel, device="cuda").to(dt)
             if op == "all_reduce":
-                fn = lambda: dist.all_reduce(x)  # noqa: E731
+                fn = lambda: dist.all_reduce(x, group=grp)  # noqa: E731
             elif op == "reduce_scatter":
                 out = torch.empty(numel // n, device="cuda", dtype=dt)
-                fn = lambda: dist.reduce_scatter_tensor(out, x)  # noqa: E731
+                fn = lambda: dist.reduce_scatter_tensor(out, x, group=grp)  # noqa: E731
             elif op == "all_gather":
                 part = torch.randn(numel // n, device="cuda").to(dt)
-                fn = lambda: dist.all_gather_into_tensor(x, part)  # noqa: E731
+                fn = lambda: dist.all_gather_into_tensor(x, part, group=grp)  # noqa: E731
             elif op == "all_to_all":
                 out = torch.empty_like(x)
-                fn = lambda: dist.all_to_all_single(out, x)  # noqa: E731
+                fn = lambda: dist.all_to_all_single(out, x, group=grp)  # noqa: E731
             else:
                 raise ValueError(op)
             for _ in range(args.warmup):
@@ -104,6 +131,7 @@ def main():
                                   "us": round(sec * 1e6, 1), "algbw_GBps": round(alg, 1),
                                   "busbw_GBps": round(bus, 1),
                                   "links_equiv": round(bus / args.link_GBps, 2),
+                                  "ctas": list(budget) if budget else None,
                                   "rccl_env": {k: v for k, v in os.environ.items()
                                                if k.startswith(("NCCL_", "RCCL_"))}}),
                       flush=True)
