@@ -82,6 +82,7 @@ int fx_gemm(int, int, int, int, int, int, int, const void*, long, const void*, l
             const void*, void*, long, int, hipStream_t, float*, float*);
 long fx_gemm_ws_bytes(int, int, int, int);
 void fx_gemm_set_variant(int);
+void fx_gemm5_set_stage(int);
 int fx_decode_gemv(int, int, int, int, int, const void*, long, const void*, long, const void*,
                    const void*, long, void*, long, void*, void*, const long*, int, int, int,
                    const void*, const void*, float, hipStream_t);
@@ -313,6 +314,7 @@ PYBIND11_MODULE(_kernels, m) {
      py::arg("st"), py::arg("sq") = 0, py::arg("ws") = 0);
   m.def("gemm_ws_bytes", &fx_gemm_ws_bytes);
   m.def("gemm_set_variant", &fx_gemm_set_variant);
+  m.def("gemm5_set_stage", &fx_gemm5_set_stage);
   // decode-time skinny GEMM with fused sub-layer epilogues (decode_gemv.hip)
   m.def("decode_gemv", [](int dt, int epi, int M, int N, int K, ptr x, long ldx, ptr w, long ldw,
                           ptr bias, ptr res, long ldres, ptr y, long ldy, ptr kc, ptr vc, ptr pos,
