@@ -81,18 +81,9 @@ int fx_softmax_bwd(int, const void*, const void*, void*, long, int, int, float, 
 int fx_gemm(int, int, int, int, int, int, int, const void*, long, const void*, long, void*, long,
             const void*, void*, long, int, hipStream_t, float*, float*);
 long fx_gemm_ws_bytes(int, int, int, int);
-void fx_gemm_set_variant(int);
-void fx_gemm5_set_stage(int);
 int fx_decode_gemv(int, int, int, int, int, const void*, long, const void*, long, const void*,
                    const void*, long, void*, long, void*, void*, const long*, int, int, int,
                    const void*, const void*, float, hipStream_t);
-int fx_decode_layer(int, int, int, int, int, int, int, int, const void*, void*, void*, float*,
-                    void*, void*, const void*, const void*, const void*, const void*, const void*,
-                    const void*, const void*, const void*, const void*, const void*, const void*,
-                    const void*, void*, void*, const long*, const int*, float, float, float,
-                    unsigned*, unsigned, int*, hipStream_t);
-int fx_decode_layer_grid();
-int fx_decode_layer_barriers();
 void fx_set_dropout_salt(const void*);
 void fx_set_adamw_lr_ptr(const void*);
 int fx_comm_max_world();
@@ -313,8 +304,6 @@ PYBIND11_MODULE(_kernels, m) {
      py::arg("ldc"), py::arg("bias"), py::arg("aux"), py::arg("ldaux"), py::arg("beta"),
      py::arg("st"), py::arg("sq") = 0, py::arg("ws") = 0);
   m.def("gemm_ws_bytes", &fx_gemm_ws_bytes);
-  m.def("gemm_set_variant", &fx_gemm_set_variant);
-  m.def("gemm5_set_stage", &fx_gemm5_set_stage);
   // decode-time skinny GEMM with fused sub-layer epilogues (decode_gemv.hip)
   m.def("decode_gemv", [](int dt, int epi, int M, int N, int K, ptr x, long ldx, ptr w, long ldw,
                           ptr bias, ptr res, long ldres, ptr y, long ldy, ptr kc, ptr vc, ptr pos,
@@ -324,24 +313,6 @@ PYBIND11_MODULE(_kernels, m) {
                           ldy, P(kc), P(vc), reinterpret_cast<const long*>(pos), heads, head_dim,
                           maxlen, CP(ln_w), CP(ln_b), ln_eps, S(st));
   });
-  // one persistent launch per decoder layer (decode_layer.hip); args as a dict
-  // of pointers / ints / floats to keep the call readable
-  m.def("decode_layer", [](py::dict d) {
-    auto I = [&](const char* k) { return d[k].cast<long>(); };
-    auto Fl = [&](const char* k) { return d[k].cast<float>(); };
-    auto Pt = [&](const char* k) { return reinterpret_cast<void*>(d[k].cast<ptr>()); };
-    return fx_decode_layer(
-        (int)I("dt"), (int)I("M"), (int)I("h"), (int)I("ffn"), (int)I("heads"), (int)I("hd"),
-        (int)I("maxlen"), (int)I("nsplit"), Pt("x"), Pt("xout"), Pt("q"),
-        reinterpret_cast<float*>(Pt("apart")), Pt("x2"), Pt("f"), Pt("ln1w"), Pt("ln1b"),
-        Pt("wqkv"), Pt("bqkv"), Pt("wo"), Pt("bo"), Pt("ln2w"), Pt("ln2b"), Pt("w1"), Pt("b1"),
-        Pt("w2"), Pt("b2"), Pt("kc"), Pt("vc"), reinterpret_cast<const long*>(Pt("pos")),
-        reinterpret_cast<const int*>(Pt("lens")), Fl("eps1"), Fl("eps2"), Fl("scale"),
-        reinterpret_cast<unsigned*>(Pt("bar")), (unsigned)I("bar_base"),
-        reinterpret_cast<int*>(Pt("err")), S(d["st"].cast<ptr>()));
-  });
-  m.def("decode_layer_grid", &fx_decode_layer_grid);
-  m.def("decode_layer_barriers", &fx_decode_layer_barriers);
   // graph mode: device-resident dropout salt / AdamW learning rate (0 = off)
   m.def("set_dropout_salt", [](ptr p) { fx_set_dropout_salt(CP(p)); });
   m.def("set_adamw_lr_ptr", [](ptr p) { fx_set_adamw_lr_ptr(CP(p)); });

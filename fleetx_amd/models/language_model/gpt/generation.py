@@ -18,7 +18,6 @@ MI355X design (K18/K19):
 * per-token attention uses the split-free decode kernel
   (``ops.decode_attention``) that streams the cache once.
 """
-import math
 import os
 import torch
 import torch.nn.functional as F
@@ -135,7 +134,6 @@ class KVCache:
                   for _ in range(num_layers)]
         self.v = [torch.zeros_like(t) for t in self.k]
         self.max_len = max_len
-        self.persistent = None  # _PersistentLayers workspace (one launch per layer)
 
 
 def _layer_prefill(layer, x, cache, li, lens):
@@ -215,85 +213,6 @@ def _layer_decode_fused(layer, x, cache, li, pos, lens_after):
         f = G.decode_linear(layer.ln2(x2), mlp.fc1.weight, mlp.fc1.bias, G.GV_GELU)
     out = G.decode_linear(f, mlp.fc2.weight, mlp.fc2.bias, G.GV_RES, res=x2)
     return out.view(B, 1, h)
-
-
-class _PersistentLayers:
-    """Workspace of the one-launch-per-layer decode kernel
-    (csrc/kernels/decode_layer.hip): the layer's five phases (LN1 + QKV + cache
-    append, split-K attention, combine + out-proj + residual, LN2 + FC1 + GeLU,
-    FC2 + residual) separated by grid barriers instead of kernel boundaries.
-    Static buffers (HIP-graph capturable); the barrier counter is zeroed at the
-    start of every decode step and layer ``li`` counts from ``li x 4 x grid``.
-
-    Opt-in (``FLEETX_DECODE_PERSISTENT=1``): measured 3x SLOWER than the graphed
-    per-op decode step (1.3B: 3.41 vs 1.09 ms/token; 6.7B: 7.64 vs 3.23), since a
-    grid barrier across the 8 XCDs costs 5-11 us against 1.55 us for a kernel
-    boundary inside a graph (tools/barrier_lab, profiles/r3_decl).  Kept as the
-    tested single-launch layer for future barrier work."""
-
-    def __init__(self, B, h, ffn, heads, hd, maxlen, dtype, device):
-        from ....ops import _lib
-        k = _lib.kernels()
-        self.k = k
-        self.grid = k.decode_layer_grid()
-        self.nbar = k.decode_layer_barriers()
-        # attention items (row, head, split) ~ one per workgroup, >= 16 keys each
-        self.nsplit = max(1, min(self.grid // max(1, B * heads), -(-maxlen // 16)))
-        self.B, self.h, self.ffn, self.heads, self.hd, self.maxlen = B, h, ffn, heads, hd, maxlen
-        self.dt = _lib.dt_code(dtype)
-        mk = lambda *shape: torch.empty(*shape, dtype=dtype, device=device)  # noqa: E731
-        self.q, self.x2, self.f = mk(B, h), mk(B, h), mk(B, ffn)
-        self.out = [mk(B, h), mk(B, h)]
-        self.apart = torch.empty(B * heads * self.nsplit * (hd + 2), dtype=torch.float32,
-                                 device=device)
-        self.bar = torch.zeros(1, dtype=torch.int32, device=device)
-        self.err = torch.zeros(1, dtype=torch.int32, device=device)
-
-    @staticmethod
-    def supported(gen, B):
-        if os.environ.get("FLEETX_DECODE_PERSISTENT", "0") != "1" or topo.mp_world_size() != 1:
-            return False
-        cfg = gen.gpt.cfg
-        h, hd = cfg.hidden_size, cfg.head_dim
-        l0 = gen.gpt.layers[0]
-        p = next(gen.parameters())
-        return (p.is_cuda and p.dtype in (torch.bfloat16, torch.float16) and B <= 4
-                and h % 1024 == 0 and cfg.ffn_hidden_size % 1024 == 0 and hd in (64, 128)
-                and _fusable(l0) and l0.attn.qkv_proj.bias is not None
-                and l0.ln1.bias is not None and l0.ln2.bias is not None)
-
-    def begin_step(self):
-        self.bar.zero_()
-
-    def layer(self, li, layer, x2d, cache, pos, lens_after):
-        from ....ops import _lib
-        attn, mlp = layer.attn, layer.mlp
-        out = self.out[li % 2]
-        d = {"dt": self.dt, "M": x2d.shape[0], "h": self.h, "ffn": self.ffn,
-             "heads": self.heads, "hd": self.hd, "maxlen": cache.max_len, "nsplit": self.nsplit,
-             "x": x2d.data_ptr(), "xout": out.data_ptr(), "q": self.q.data_ptr(),
-             "apart": self.apart.data_ptr(), "x2": self.x2.data_ptr(), "f": self.f.data_ptr(),
-             "ln1w": layer.ln1.weight.data_ptr(), "ln1b": layer.ln1.bias.data_ptr(),
-             "wqkv": attn.qkv_proj.weight.data_ptr(), "bqkv": attn.qkv_proj.bias.data_ptr(),
-             "wo": attn.out_proj.weight.data_ptr(), "bo": attn.out_proj.bias.data_ptr(),
-             "ln2w": layer.ln2.weight.data_ptr(), "ln2b": layer.ln2.bias.data_ptr(),
-             "w1": mlp.fc1.weight.data_ptr(), "b1": mlp.fc1.bias.data_ptr(),
-             "w2": mlp.fc2.weight.data_ptr(), "b2": mlp.fc2.bias.data_ptr(),
-             "kc": cache.k[li].data_ptr(), "vc": cache.v[li].data_ptr(),
-             "pos": pos.data_ptr(), "lens": lens_after.data_ptr(),
-             "eps1": float(layer.ln1.eps), "eps2": float(layer.ln2.eps),
-             "scale": 1.0 / math.sqrt(self.hd), "bar": self.bar.data_ptr(),
-             "bar_base": li * self.nbar * self.grid, "err": self.err.data_ptr(),
-             "st": _lib.stream()}
-        rc = self.k.decode_layer(d)
-        if rc != 0:
-            raise RuntimeError("decode_layer launch refused (rc %d)" % rc)
-        return out
-
-    def check(self):
-        if int(self.err.item()) != 0:
-            raise RuntimeError("persistent decode layer: a grid barrier timed out (not every "
-                               "workgroup could be resident); set FLEETX_DECODE_PERSISTENT=0")
 
 
 class _GraphedDecodeStep:
@@ -385,15 +304,6 @@ class GPTForGeneration(torch.nn.Module):
                           cur[:, None], self.gpt.embeddings.position_embeddings, 0) \
             if topo.mp_world_size() == 1 else self.gpt.embeddings(nxt[:, None], cur[:, None])
         after = (cur + 1).to(torch.int32)
-        runner = getattr(cache, "persistent", None)
-        if runner is not None:  # one launch per decoder layer
-            runner.begin_step()
-            h = x.reshape(x.shape[0], -1)
-            cur_c = cur.contiguous()
-            for li, layer in enumerate(self.gpt.layers):
-                h = runner.layer(li, layer, h, cache, cur_c, after)
-            x = self.gpt.final_ln(h.view(x.shape[0], 1, -1))
-            return self._logits(x[:, 0])
         fused = self.fused_decode and x.is_cuda and x.shape[0] <= 16
         for li, layer in enumerate(self.gpt.layers):
             y = _layer_decode_fused(layer, x, cache, li, cur, after) \
@@ -433,10 +343,6 @@ class GPTForGeneration(torch.nn.Module):
         p = next(self.parameters())
         attn0 = self.gpt.layers[0].attn
         cache = KVCache(len(self.gpt.layers), B, total, attn0.heads, attn0.head_dim, p.dtype, dev)
-        if self.fused_decode and _PersistentLayers.supported(self, B):
-            cache.persistent = _PersistentLayers(B, cfg.hidden_size, cfg.ffn_hidden_size,
-                                                 attn0.heads, attn0.head_dim, total, p.dtype,
-                                                 dev)
         gen = None
         if seed is not None:
             gen = torch.Generator(device=dev)
@@ -499,8 +405,6 @@ class GPTForGeneration(torch.nn.Module):
             logits = graphed(nxt, cur) if graphed is not None else \
                 self._decode_step(nxt, cur, cache)
             cur = cur + 1
-        if getattr(cache, "persistent", None) is not None:
-            cache.persistent.check()
         if not out_tokens:
             return torch.zeros(B, 0, dtype=torch.long, device=dev), scores
         return torch.stack(out_tokens, 1), scores

@@ -292,10 +292,7 @@ def layer_norm_keep_input(x, weight, bias, eps=1e-5):
     """``(x', LN(x))`` with ``x'`` an alias of ``x`` to use as the residual:
     the gradient that reaches ``x'`` enters the LayerNorm backward kernel as
     its ``ds_in`` instead of autograd adding the two branch gradients of
-    ``x`` in a separate pass (pre-LN blocks: ``x + f(LN(x))``).
-    ``FLEETX_LN_KEEP_INPUT=0``: plain LayerNorm (A/B)."""
-    if os.environ.get("FLEETX_LN_KEEP_INPUT", "1") == "0":
-        return x, layer_norm(x, weight, bias, eps)
+    ``x`` in a separate pass (pre-LN blocks: ``x + f(LN(x))``)."""
     return _AddLayerNorm.apply(x, None, None, weight, bias, eps, 0.0, 0, True)
 
 

@@ -303,11 +303,10 @@ class FusedAdamW(FlatOptimizer):
         # profiles/r2_final/adamw_overlap_grid.txt).  0 = uncapped.
         grid = int(os.environ.get("FLEETX_ADAMW_OVERLAP_GRID", str(self.overlap_grid)))
         wide = int(os.environ.get("FLEETX_ADAMW_OVERLAP_WIDE", str(int(self.overlap_wide))))
-        # FLEETX_ADAMW_OVERLAP_HEAD=n: the first n units (root = embeddings,
-        # then layer 0, ...) run uncapped, as they gate the first forward
-        # kernels; measured neutral on 6.7B / 1.3B (profiles/r3_adamw/
-        # head_ab.txt), so capped from the start by default
-        head = int(os.environ.get("FLEETX_ADAMW_OVERLAP_HEAD", "0"))
+        # (running the first units -- embeddings, layer 0 -- uncapped because
+        # they gate the first forward kernels measured neutral on 6.7B / 1.3B:
+        # profiles/r3_adamw/head_ab.txt; every unit is capped)
+        head = 0
         if getattr(self, "_overlap_args", None) is None:
             # launch arguments per unit, built once (the flat buffers never
             # move): the per-step host cost is then one bound call per range

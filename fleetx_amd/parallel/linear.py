@@ -19,10 +19,8 @@ axis of both row-major activations, and hipBLASLt's kernels for that "NT"
 case reach only ~1.0 PFLOP/s on gfx950.  On GPU both operands are first
 transposed to token-contiguous copies by the LDS-tiled HIP transpose
 (``ops.elementwise.transpose2d``) so the GEMM runs as "TN" (~1.35 PFLOP/s
-with fp32 accumulate; ``tools/bench_gemm.py``).  ``FLEETX_WGRAD_TN=0``
-restores the direct call.
+with fp32 accumulate; ``tools/bench_gemm.py``).
 """
-import os
 
 import torch
 import torch.nn.functional as F
@@ -40,21 +38,18 @@ def _mm_out_supported():
     return _MM_DTYPE_OUT
 
 
-_WGRAD_TN = os.environ.get("FLEETX_WGRAD_TN", "1") == "1"
-_DGRAD_TN = os.environ.get("FLEETX_DGRAD_TN", "1") == "1"
-
 
 def dgrad(dy, w):
     """``dy @ w`` (data gradient of ``F.linear(x, w)``).  On GPU the weight is
     first transposed (LDS-tiled HIP transpose, ~2 B/elt each way) so the GEMM
     runs as ``F.linear(dy, w^T)`` -- the "TN" layout hipBLASLt's tuned kernels
     cover (~1.5 vs ~1.3 PFLOP/s for the "NN" call on the GPT-3 6.7B shapes;
-    ``tools/bench_gemm.py``).  ``FLEETX_DGRAD_TN=0`` keeps the direct call.
+    ``tools/bench_gemm.py``).
 
     The transpose costs ~4 B per weight element at ~4.5 TB/s while the GEMM
     saves ~13 % of 2*M FLOPs per element at ~1.4 PFLOP/s: it pays off from
     M ~ 4.5k rows, so smaller micro-batches (pipeline schedules) keep NN."""
-    if _DGRAD_TN and dy.is_cuda and dy.dtype in (torch.bfloat16, torch.float16) \
+    if dy.is_cuda and dy.dtype in (torch.bfloat16, torch.float16) \
             and w.dtype == dy.dtype and w.dim() == 2 and w.shape[0] % 8 == 0 \
             and w.shape[1] % 8 == 0 and dy.numel() // dy.shape[-1] >= 6144:
         from ..ops.elementwise import transpose2d
@@ -69,7 +64,7 @@ def _fused(p):
 def _tn_operands(dy2, x2, colsum=None):
     """(dy2^T, x2) as (token-contiguous dyT, xT^T view) when the TN path applies;
     ``colsum`` = (fp32 target, accumulate) takes dy2's column sums on the way."""
-    if not (_WGRAD_TN and dy2.is_cuda and dy2.dtype in (torch.bfloat16, torch.float16)
+    if not (dy2.is_cuda and dy2.dtype in (torch.bfloat16, torch.float16)
             and x2.dtype == dy2.dtype):
         return None
     from ..ops.elementwise import transpose2d

@@ -130,52 +130,3 @@ def test_fused_decode_step_matches_unfused():
     assert _rel(outs[1][0], outs[0][0]) < 2e-2
     for a, b in zip(outs[0][1] + outs[0][2], outs[1][1] + outs[1][2]):
         assert _rel(b, a) < 2e-2
-
-
-@pytest.mark.parametrize("B,heads,hd", [(1, 8, 128), (3, 16, 64), (4, 8, 128)])
-def test_persistent_decode_layer_matches_fused(B, heads, hd, monkeypatch):
-    """One persistent launch per decoder layer (csrc/kernels/decode_layer.hip:
-    grid barriers between LN1+QKV+cache append, split-K attention,
-    combine+out-proj, LN2+FC1+GeLU, FC2) against the five-kernel fused decode
-    layer: logits and every K/V cache entry, on cache lengths that differ per
-    row (one row at position 0)."""
-    from fleetx_amd.models.language_model.gpt.model import GPTConfig, GPTForPretraining
-    from fleetx_amd.models.language_model.gpt import generation as gmod
-    torch.manual_seed(1)
-    h = heads * hd
-    cfg = GPTConfig(vocab_size=1024, hidden_size=h, num_layers=3, num_attention_heads=heads,
-                    max_position_embeddings=256, hidden_dropout_prob=0.0,
-                    attention_probs_dropout_prob=0.0, dtype=torch.bfloat16)
-    model = GPTForPretraining(cfg).cuda().eval()
-    with torch.no_grad():  # non-trivial biases / LN affine
-        for n, prm in model.named_parameters():
-            if prm.ndim == 1:
-                prm.add_(0.1 * torch.randn_like(prm))
-    gen = gmod.GPTForGeneration(model, {"fused_decode": True}).eval()
-    assert not gmod._PersistentLayers.supported(gen, B)  # opt-in: slower than the graph
-    monkeypatch.setenv("FLEETX_DECODE_PERSISTENT", "1")
-    assert gmod._PersistentLayers.supported(gen, B)
-    outs = []
-    for persistent in (False, True):
-        cache = gmod.KVCache(cfg.num_layers, B, 200, heads, hd, torch.bfloat16, DEV)
-        g = torch.Generator(device=DEV).manual_seed(9)
-        for L in range(cfg.num_layers):
-            cache.k[L].normal_(generator=g)
-            cache.v[L].normal_(generator=g)
-        if persistent:
-            cache.persistent = gmod._PersistentLayers(B, h, 4 * h, heads, hd, 200, torch.bfloat16,
-                                                      DEV)
-        nxt = torch.randint(0, 1024, (B,), device=DEV, generator=g)
-        cur = torch.tensor([3, 0, 199, 77][:B], device=DEV)
-        lgs = []
-        with torch.no_grad():
-            for step in range(3):  # consecutive tokens: the barrier counter restarts each step
-                lgs.append(gen._decode_step(nxt, cur + step * (cur < 197), cache).float())
-        torch.cuda.synchronize()
-        if persistent:
-            cache.persistent.check()
-        outs.append((lgs, [c.clone() for c in cache.k], [c.clone() for c in cache.v]))
-    for a, b in zip(outs[0][0], outs[1][0]):
-        assert _rel(b, a) < 2e-2, _rel(b, a)
-    for a, b in zip(outs[0][1] + outs[0][2], outs[1][1] + outs[1][2]):
-        assert _rel(b, a) < 2e-2

@@ -33,9 +33,6 @@ def main():
     ap.add_argument("--hidden", type=int, default=4096)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="", help="comma list of case names")
-    ap.add_argument("--variants", default="", help="comma list of HIP GEMM K-loop variants to A/B")
-    ap.add_argument("--stages", default="", help="comma list of gemm5 K-loop stagings to A/B "
-                                                "(0 = LDS-DMA, 1 = VGPR)")
     a = ap.parse_args()
     from fleetx_amd.ops.elementwise import transpose2d
     from fleetx_amd.ops import gemm as G
@@ -83,23 +80,9 @@ def main():
             "hip_dgrad_dgelu": lambda: G.linear_dgrad(dy, w, act_input=hpre),
             "hip_wgrad_f32acc": lambda: G.linear_wgrad(dy, x, dw32, True),
         }
-        variants = [int(v) for v in a.variants.split(",")] if a.variants else [None]
-        stages = [int(v) for v in a.stages.split(",")] if a.stages else [None]
-        items = []
         for k, fn in cases.items():
             if a.only and k not in a.only.split(","):
                 continue
-            if k.startswith("hip_"):
-                items += [(k + ("" if v is None else "_v%d" % v) + ("" if g is None else "_s%d" % g),
-                           fn, v, g) for v in variants for g in stages]
-            else:
-                items.append((k, fn, None, None))
-        from fleetx_amd.ops import _lib
-        for k, fn, v, g in items:
-            if v is not None:
-                _lib.kernels().gemm_set_variant(v)
-            if g is not None:
-                _lib.kernels().gemm5_set_stage(g)
             ms = timeit(fn, a.iters)
             # TFLOP/s of the GEMM (for transposes: us per call)
             res[k] = round(ms * 1e3, 1) if k.startswith("transpose") else round(fl / ms / 1e9, 1)

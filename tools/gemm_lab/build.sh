@@ -8,11 +8,11 @@ cd "$(dirname "$0")"
 mkdir -p bin
 for abl in ${ABLS:-0 1 2 3}; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -DFX_GEMM_ABL=$abl $EXTRA \
-    -o bin/gemm_lab_abl$abl gemm_lab.cpp ../../csrc/kernels/gemm.hip ../../csrc/kernels/gemm5.hip &
+    -o bin/gemm_lab_abl$abl gemm_lab.cpp gemm_legacy.hip ../../csrc/kernels/gemm5.hip &
 done
 if [ -z "$ABLS" ]; then
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -DFX_GEMM_STAMP=1 \
-  -o bin/gemm_lab_stamp gemm_lab.cpp ../../csrc/kernels/gemm.hip ../../csrc/kernels/gemm5.hip &
+  -o bin/gemm_lab_stamp gemm_lab.cpp gemm_legacy.hip ../../csrc/kernels/gemm5.hip &
 fi
 wait
 ls -la bin

@@ -55,9 +55,7 @@ def set_geometry(tag):
     fb = 128 if nf == 8 else 64
     n = 4 * nf  # registers per (operand, k-step) fragment set
     GEO.clear()
-    # stage: first of the 8 nf VGPRs that hold one K-tile's staged pieces
-    # (VGPR-staged loop only): v[64:127] (T256) / v[32:63] (T128)
-    GEO.update(tag=tag, nf=nf, buf=2 * (32 * nf) * 128, stage=fb // 2,
+    GEO.update(tag=tag, nf=nf, buf=2 * (32 * nf) * 128,
                frag_base={("A", 0): fb, ("A", 1): fb + n, ("B", 0): fb + 2 * n,
                           ("B", 1): fb + 3 * n})
 
@@ -290,291 +288,6 @@ def body_with(st, la, lb, dt, kind, read_gap, dma_gap):
     return st.lines, st.pending
 
 
-# ---------------------------------------------------------------------------
-# VGPR-staged K-loop (FX_G6_*): each wave moves its 2 nf pieces (1 KiB = 16 B
-# per lane) of a K-tile HBM/L2 -> VGPR with buffer_load_dwordx4 and VGPR ->
-# LDS with ds_write_b128, instead of LDS-DMA (whose issue stalls the wave
-# for 60-185 cycles among MFMAs and measured 20-30 % of the loop:
-# profiles/r3_gemm/ablations_v5.log).  The LDS images, fragment reads and
-# per-lane source offsets are the DMA loop's (a piece lands where its DMA
-# would: wave base + 1 KiB * piece + 16 B * lane).
-#
-# Per K-tile t (4 segments of nf^2/2 MFMAs, ONE barrier):
-#   S1  k0 rows 0..h-1 + B k1 reads (tile t)
-#   S2  k0 rows h..nf-1 + A k1 reads; lgkmcnt(0) + s_barrier: every wave is
-#       done with tile t's buffer, and every wave's writes of tile t+1 (S3
-#       of t-1) are complete
-#   S3  k1 rows 0..h-1 + ds_write of tile t+2 into tile t's buffer (from the
-#       stage VGPRs), each write followed (after `lag` gaps) by the load of
-#       the same piece of tile t+3 into the same VGPRs
-#   S4  k1 rows h..nf-1 + tile t+1 k0 reads (+ late loads)
-# A piece's load is in flight for a whole K-tile (~2k cycles) before its
-# write needs it; the counted vmcnt waits come from a VMEM scoreboard.
-class VStream(Stream):
-    def __init__(self):
-        super().__init__()
-        self.vpend = []
-
-    def vload(self, key, text):
-        self.lines.append(text)
-        self.vpend.append(key)
-
-    def vneed(self, key):
-        idx = self.vpend.index(key)
-        n = len(self.vpend) - 1 - idx
-        assert n <= 63
-        self.lines.append("s_waitcnt vmcnt(%d)" % n)
-        self.vpend = self.vpend[idx + 1:]
-
-    def write(self, text):
-        self.lines.append(text)
-        self.pending.append(("w",))
-
-
-def pieces():
-    nf = GEO["nf"]
-    return [("B", u) for u in range(nf)] + [("A", u) for u in range(nf)]
-
-
-def stage_reg(p):
-    return GEO["stage"] + 4 * p
-
-
-def load_text(op, u, dst):
-    return "buffer_load_dwordx4 %s, %%[vo%s%d], %%[rs%s], %%[so%s] offen" % (
-        vreg(dst, 4), op, u, op, op)
-
-
-def write_text(op, u, src):
-    off = (GEO["buf"] // 2 if op == "B" else 0) + 1024 * u
-    return "ds_write_b128 %%[wb], %s offset:%d" % (vreg(src, 4), off)
-
-
-def segment_at(dt, st, s, rows, plan, close=None):
-    """MFMAs of k-step s for fragment rows `rows`; plan[gap] = actions issued
-    after that gap's MFMA: ('read', (key, text)) | ('write', op, u, src,
-    need_key) | ('load', key, text).  `close`: 'lgkm0' drains LDS and emits
-    s_barrier after the last MFMA."""
-    mf = [(s, i, j) for i in rows for j in range(GEO["nf"])]
-    for p, (ss, i, j) in enumerate(mf):
-        if close == "lgkm0" and p == len(mf) - 1:
-            st.drain()
-        mfma(dt, st, ss, i, j)
-        for act in plan.get(p, []):
-            if act[0] == "read":
-                st.read(act[1][0], act[1][1])
-            elif act[0] == "write":
-                _, op, u, src, need = act
-                if need is not None:
-                    st.vneed(need)
-                st.write(write_text(op, u, src))
-            else:
-                st.vload(act[1], act[2])
-    if close == "lgkm0":
-        st.emit("s_barrier")
-
-
-def spread(items, ngaps, start=0, gap=1):
-    plan = {}
-    for n, it in enumerate(items):
-        plan.setdefault(min(ngaps - 2, start + n * gap), []).append(it)
-    return plan
-
-
-# Schedule knobs of the VGPR-staged loop (per geometry, see main()):
-#   wspan    segments (from S3) the 2 nf piece writes are spread over (1|2)
-#   lag      gaps from a piece's write to the load that refills its VGPRs
-#            (mod the body: a load past the body end is issued in the next
-#            body's S1/S2, before that body writes the piece)
-#   stagger  per-wave shift (gaps) of the loads: the four waves leave the
-#            barrier in step, so unshifted they queue their loads at the CU's
-#            address unit together (one copy of the loop per wave)
-VCFG = {}
-
-
-def v_positions(w):
-    """(write gap, load gap) of every piece for wave w, body-relative."""
-    nf = GEO["nf"]
-    seg = (nf // 2) * nf
-    total = 4 * seg
-    n = 2 * nf
-    span = VCFG["wspan"] * seg
-    out = []
-    for p in range(n):
-        wg = 2 * seg + (p * span) // n
-        lg = (wg + VCFG["lag"] + VCFG["stagger"] * w) % total
-        out.append((wg, lg))
-    return out
-
-
-def body_v(st, la, lb, dt, kind, w):
-    """kind: 'full' (writes t+2, loads t+2 / t+3, reads t+1), 'wonly'
-    (writes t+2, loads of t+2 only), 'nodma' (reads t+1), 'last'."""
-    lay = {"A": la, "B": lb}
-    nf, X = GEO["nf"], "0x%x" % GEO["buf"]
-    h = nf // 2
-    seg = h * nf
-    ps = pieces()
-
-    def reads(op, s, which):
-        return [("read", r) for i in range(nf) for r in read_ops(lay[op], op, s, i, which)]
-
-    last = kind == "last"
-    plan = {}
-
-    def put(g, act):
-        plan.setdefault(g, []).append(act)
-
-    for n, r in enumerate(reads("B", 1, "cur")):
-        put(min(seg - 2, n), r)
-    for n, r in enumerate(reads("A", 1, "cur")):
-        put(seg + min(seg - 2, n), r)
-    if not last:
-        for n, r in enumerate(reads("B", 0, "nxt") + reads("A", 0, "nxt")):
-            put(3 * seg + min(seg - 2, n), r)
-    if kind in ("full", "wonly"):
-        pos = v_positions(w)
-        # one soffset per operand: every load of a body is for the same tile
-        # (all wrapped -> t+2 with so at t+2, or all after their writes ->
-        # t+3 with so at t+3)
-        assert len(set(lg >= wg for wg, lg in pos)) == 1, "mixed load tiles in one body"
-        for n, ((op, u), (wg, lg)) in enumerate(zip(ps, pos)):
-            put(wg, ("write", op, u, stage_reg(n), ("ld", n, 2)))
-            same = lg >= wg
-            if kind == "full" or not same:
-                put(lg, ("load", ("ld", n, 3 if same else 2), load_text(op, u, stage_reg(n))))
-    order = {"read": 0, "write": 1, "load": 2}
-    for s_ in range(4):
-        sp = {g - s_ * seg: sorted(a, key=lambda x: order[x[0]])
-              for g, a in plan.items() if s_ * seg <= g < (s_ + 1) * seg}
-        close = "lgkm0" if (s_ == 1 and not last) else None
-        segment_at(dt, st, s_ // 2, range(0, h) if s_ % 2 == 0 else range(h, nf), sp, close=close)
-    if last:
-        st.emit("s_nop 15")
-        st.emit("s_nop 15")
-        return
-    for op in "AB":
-        if lay[op] == KC:
-            st.emit("v_xor_b32 %%[r%s_cur], %s, %%[r%s_cur]" % (op, X, op))
-            st.emit("v_xor_b32 %%[r%s_nxt], %s, %%[r%s_nxt]" % (op, X, op))
-        else:
-            for wn in ("curlo", "curhi", "nxtlo", "nxthi"):
-                st.emit("v_xor_b32 %%[r%s_%s], %s, %%[r%s_%s]" % (op, wn, X, op, wn))
-        if kind == "full":
-            st.emit("s_add_u32 %%[so%s], %%[so%s], %%[ks%s]" % (op, op, op))
-    if kind in ("full", "wonly"):
-        st.emit("v_xor_b32 %%[wb], %s, %%[wb]" % X)
-    # loads issued this body are for the tile one body closer next time
-    st.vpend = [(k[0], k[1], k[2] - 1) for k in st.vpend]
-
-
-def steady_state(la, lb, dt, w):
-    """Fixed point of the (lgkm, vmem) scoreboards at the loop-body start."""
-    pend, vpend = [], [("ld", n, 2) for n in range(2 * GEO["nf"])]
-    for _ in range(6):
-        b = VStream()
-        b.pending, b.vpend = list(pend), list(vpend)
-        body_v(b, la, lb, dt, "full", w)
-        if b.pending == pend and b.vpend == vpend:
-            return pend, vpend
-        pend, vpend = b.pending, b.vpend
-    raise AssertionError("loop body scoreboard has no fixed point")
-
-
-def generate_v_wave(la, lb, dt, w):
-    lay = {"A": la, "B": lb}
-    nf, X = GEO["nf"], "0x%x" % GEO["buf"]
-    ps = pieces()
-    carried, vcarried = steady_state(la, lb, dt, w)
-    st = VStream()
-    fb = GEO["frag_base"][("A", 0)]
-
-    def adv():
-        for op in "BA":
-            st.emit("s_add_u32 %%[so%s], %%[so%s], %%[ks%s]" % (op, op, op))
-
-    # prologue: tile 0 -> stage VGPRs, tile 1 -> fragment VGPRs (free until
-    # the first fragment reads), write tile 0, the steady state's tile-2
-    # loads (same pieces, same order), write tile 1
-    for n, (op, u) in enumerate(ps):
-        st.vload(("p", n, 0), load_text(op, u, stage_reg(n)))
-    adv()
-    for n, (op, u) in enumerate(ps):
-        st.vload(("p", n, 1), load_text(op, u, fb + 4 * n))
-    adv()
-    for n, (op, u) in enumerate(ps):
-        st.vneed(("p", n, 0))
-        st.write(write_text(op, u, stage_reg(n)))
-    st.emit("v_xor_b32 %%[wb], %s, %%[wb]" % X)
-    for key in vcarried:
-        assert key[2] == 2, key
-        op, u = ps[key[1]]
-        st.vload(key, load_text(op, u, stage_reg(key[1])))
-    if vcarried:
-        adv()   # the loop's loads are for tile t+3
-    for n, (op, u) in enumerate(ps):
-        st.vneed(("p", n, 1))
-        st.write(write_text(op, u, fb + 4 * n))
-    st.emit("v_xor_b32 %%[wb], %s, %%[wb]" % X)
-    st.drain()
-    st.emit("s_barrier")
-    for op in "BA":
-        for i in range(nf):
-            for key, text in read_ops(lay[op], op, 0, i, "nxt"):
-                st.read(key, text)
-    for op in "AB":
-        if lay[op] == KC:
-            st.emit("v_xor_b32 %%[r%s_nxt], %s, %%[r%s_nxt]" % (op, X, op))
-        else:
-            st.emit("v_xor_b32 %%[r%s_nxtlo], %s, %%[r%s_nxtlo]" % (op, X, op))
-            st.emit("v_xor_b32 %%[r%s_nxthi], %s, %%[r%s_nxthi]" % (op, X, op))
-    # the loop's waits assume the steady state; the fragment reads above are
-    # a shorter queue, so drain them (once per tile)
-    st.drain()
-    assert st.vpend == vcarried
-    out = list(st.lines)
-
-    def body(kind, pend, vpend):
-        b = VStream()
-        b.pending, b.vpend = list(pend), list(vpend)
-        body_v(b, la, lb, dt, kind, w)
-        return b
-
-    out.append("s_cmp_eq_u32 %[cnt], 0")
-    out.append("s_cbranch_scc1 L_tail%d_%%=" % w)
-    full = body("full", carried, vcarried)
-    out.append("L_loop%d_%%=:" % w)
-    out += full.lines
-    out.append("s_sub_u32 %[cnt], %[cnt], 1")
-    out.append("s_cmp_lg_u32 %[cnt], 0")
-    out.append("s_cbranch_scc1 L_loop%d_%%=" % w)
-    out.append("L_tail%d_%%=:" % w)
-    b = body("wonly", carried, vcarried)
-    out += b.lines
-    b = body("nodma", b.pending, b.vpend)
-    out += b.lines
-    b = body("last", b.pending, b.vpend)
-    out += b.lines
-    return out
-
-
-def generate_v(la, lb, dt):
-    nw = 4 if VCFG["stagger"] else 1
-    if nw == 1:
-        return generate_v_wave(la, lb, dt, 0)
-    out = []
-    for w in range(1, nw):
-        out.append("s_cmp_eq_u32 %%[wid], %d" % w)
-        out.append("s_cbranch_scc1 L_w%d_%%=" % w)
-    for w in range(nw):
-        out.append("L_w%d_%%=:" % w)
-        out += generate_v_wave(la, lb, dt, w)
-        if w + 1 < nw:
-            out.append("s_branch L_end_%=")
-    out.append("L_end_%=:")
-    return out
-
-
 def c_string(lines):
     return "\n".join('  "%s\\n"' % l for l in lines)
 
@@ -583,15 +296,16 @@ ABL = set(a for a in os.environ.get("FX_GEN_ABL", "").split(",") if a)
 
 
 def ablate(lines):
-    """Lab-only ablations (FX_GEN_ABL=novm,nodma,nobar,nolds,nowr): timing
-    builds with a class of instructions removed; their results are wrong."""
+    """Lab-only ablations (FX_GEN_ABL=novm,nodma,nobar,nolds): timing builds
+    with a class of instructions removed; their results are wrong.  (A
+    VGPR-staged variant of this loop -- buffer_load -> VGPR -> ds_write, one
+    barrier per K-tile -- measured 5-10 % slower on every shape:
+    profiles/r4_gemm_vgpr/.)"""
     out = []
     for l in lines:
         if "novm" in ABL and l.startswith("s_waitcnt vmcnt"):
             continue
         if "nodma" in ABL and l.startswith("buffer_load"):
-            continue
-        if "nowr" in ABL and l.startswith("ds_write"):
             continue
         if "nobar" in ABL and l == "s_barrier":
             continue
@@ -623,21 +337,6 @@ def main():
             for dt in ("bf16", "f16"):
                 lines = ablate(generate(la, lb, dt, read_gap, dma_gap))
                 parts.append("#define FX_G5_%s_%s_%s_%s \\\n%s\n" % (
-                    tag, names[la], names[lb], dt.upper(),
-                    " \\\n".join('  "%s\\n"' % l for l in lines)))
-    # VGPR-staged loops (gemm5.hip STG = 1); lag = gaps between a piece's
-    # write and the load that refills its VGPRs
-    def knob(name, tag, default):
-        return int(os.environ.get("FX_GEN_V%s_%s" % (name, tag), default))
-    vdef = {"T256": (2, 64, 1), "T128": (2, 16, 0)}   # (wspan, lag, stagger)
-    for tag in ("T256", "T128"):
-        set_geometry(tag)
-        VCFG.update(wspan=knob("SPAN", tag, vdef[tag][0]), lag=knob("LAG", tag, vdef[tag][1]),
-                    stagger=knob("STAGGER", tag, vdef[tag][2]))
-        for la, lb in ((KC, KC), (KC, MC), (MC, MC)):
-            for dt in ("bf16", "f16"):
-                lines = ablate(generate_v(la, lb, dt))
-                parts.append("#define FX_G6_%s_%s_%s_%s \\\n%s\n" % (
                     tag, names[la], names[lb], dt.upper(),
                     " \\\n".join('  "%s\\n"' % l for l in lines)))
     with open(path, "w") as f:
