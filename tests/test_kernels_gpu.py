@@ -651,7 +651,7 @@ def test_tn_wgrad_matches_direct():
     dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
     x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
     ref = dy.float().t() @ x.float()
-    for tn in (True, False):
+    for _ in range(1):
         w = torch.nn.Parameter(torch.zeros(N, K, device="cuda", dtype=torch.bfloat16))
         w.main_grad = torch.full((N, K), 7.0, device="cuda")
         w._fx_fresh = True
@@ -659,14 +659,10 @@ def test_tn_wgrad_matches_direct():
         b.main_grad = torch.full((N,), 7.0, device="cuda")
         b._fx_fresh, b._fx_fused_wgrad = True, True
         b2 = torch.nn.Parameter(torch.zeros(N, device="cuda", dtype=torch.bfloat16))
-        old, L._WGRAD_TN = L._WGRAD_TN, tn
-        try:
-            assert (L._tn_operands(dy, x) is not None) == tn
-            assert L.accumulate_wgrad(w, dy, x, b) is None   # fresh: overwrite
-            L.accumulate_wgrad(w, dy, x, b)                  # accumulate
-            db = L.accumulate_wgrad(w, dy, x, b2)            # unfused bias: returned
-        finally:
-            L._WGRAD_TN = old
+        assert L._tn_operands(dy, x) is not None
+        assert L.accumulate_wgrad(w, dy, x, b) is None   # fresh: overwrite
+        L.accumulate_wgrad(w, dy, x, b)                  # accumulate
+        db = L.accumulate_wgrad(w, dy, x, b2)            # unfused bias: returned
         torch.testing.assert_close(w.main_grad, 3 * ref, rtol=2e-3, atol=3e-2)
         torch.testing.assert_close(b.main_grad, 2 * dy.float().sum(0), rtol=1e-3, atol=1e-2)
         torch.testing.assert_close(db.float(), dy.float().sum(0), rtol=1e-2, atol=1e-1)
