@@ -221,10 +221,12 @@ class ErnieLMPredictionHead(nn.Module):
             self.decoder_weight = nn.Parameter(L.init_full_then_slice(
                 (vocab_size, hidden_size), std, "ernie.lm_decoder", dim=0, dtype=dtype))
             self.decoder_weight.tp_split = t > 1
+            self.decoder_weight.tp_dim = 0
         else:
             self.decoder_weight = embedding_weights
         self.decoder_bias = nn.Parameter(torch.zeros(vocab_size // t, dtype=dtype or torch.float32))
         self.decoder_bias.tp_split = t > 1
+        self.decoder_bias.tp_dim = 0
 
     def forward(self, hidden_states, masked_positions=None):
         if masked_positions is not None:

@@ -46,6 +46,7 @@ class GPTForPretrainingPipe(nn.Module):
                                        "embeddings.word.weight", dim=0, dtype=cfg.dtype)
             self.shared_word_embeddings = nn.Parameter(w)
             self.shared_word_embeddings.tp_split = hcg.mp_degree > 1
+            self.shared_word_embeddings.tp_dim = 0
             self.shared_word_embeddings.shared_embedding = True
             self.shared_word_embeddings.norm_exclude = True
         self.criterion = GPTPretrainingCriterion(cfg)

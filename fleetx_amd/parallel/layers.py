@@ -96,6 +96,7 @@ class ColumnParallelLinear(nn.Module):
                                                         name + ".weight", dim=0, dtype=dtype,
                                                         device=device))
         self.weight.tp_split = t > 1
+        self.weight.tp_dim = 0
         self.weight._fx_fused_wgrad_ok = True
         self.weight._fx_gemm_wgrad = True  # gradient from the wgrad GEMM (fused-norm partials)
         if bias:
@@ -103,6 +104,7 @@ class ColumnParallelLinear(nn.Module):
                                                           dim=0, dtype=dtype, device=device,
                                                           init="zeros"))
             self.bias.tp_split = t > 1
+            self.bias.tp_dim = 0
             # a bias applied inside linear() gets its fp32 grad from the wgrad pass
             self.bias._fx_fused_wgrad_ok = not skip_bias_add
         else:
@@ -145,6 +147,7 @@ class RowParallelLinear(nn.Module):
                                                         name + ".weight", dim=1, dtype=dtype,
                                                         device=device))
         self.weight.tp_split = t > 1
+        self.weight.tp_dim = 1
         self.weight._fx_fused_wgrad_ok = True
         self.weight._fx_gemm_wgrad = True  # gradient from the wgrad GEMM (fused-norm partials)
         if bias:
@@ -189,6 +192,7 @@ class VocabParallelEmbedding(nn.Module):
         self.weight = nn.Parameter(init_full_then_slice((vocab_size, hidden), std, name + ".weight",
                                                         dim=0, dtype=dtype, device=device))
         self.weight.tp_split = t > 1
+        self.weight.tp_dim = 0
 
     def forward(self, ids, pos_ids=None, pos_weight=None, reduce=True):
         out = ops.embedding(ids, self.weight, pos_ids, pos_weight, self.vocab_start)

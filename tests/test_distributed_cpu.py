@@ -56,6 +56,8 @@ def _train(rank, world, layout, steps=3, extra=()):
     drank = hcg.dp_rank * hcg.sharding_degree + hcg.sharding_rank
     toks = _global_batch()
     losses, norms = [], []
+    from fleetx_amd.parallel.state_gather import gather_master_state
+    master0 = gather_master_state(eng)
     for s in range(steps):
         t = toks[0, drank * local:(drank + 1) * local]
         batch = [t[:, :-1].contiguous(), torch.arange(SEQ).expand(local, SEQ).contiguous(),
@@ -63,17 +65,26 @@ def _train(rank, world, layout, steps=3, extra=()):
         loss = eng._fit_impl(batch)
         losses.append(eng._reduce_log_loss(loss, 1))
         norms.append(float(eng.optimizer.last_grad_norm))
-    return {"losses": losses, "norms": norms, "drank": drank, "mp": hcg.mp_rank, "pp": hcg.pp_rank}
+    return {"losses": losses, "norms": norms, "drank": drank, "mp": hcg.mp_rank, "pp": hcg.pp_rank,
+            "master": gather_master_state(eng), "master0": master0 if rank == 0 else None}
 
 
 def _single(extra=()):
     r = dist_utils.run(_train, 1, (1, 1, 1, 1, 0, GBS, False, 1), 3, tuple(extra))
-    return r[0]["losses"]
+    return r[0]
+
+
+class _Ref(list):
+    """Reference loss curve (a list) carrying the single-process master
+    weights before (``master0``) and after (``master``) the steps."""
 
 
 @pytest.fixture(scope="module")
 def ref_losses():
-    return _single()
+    r = _single()
+    ref = _Ref(r["losses"])
+    ref.master, ref.master0 = r["master"], r["master0"]
+    return ref
 
 
 def _avg_over_data(results):
@@ -88,6 +99,26 @@ def _check(results, ref, tol=2e-4):
     got = _avg_over_data(results)
     for a, b in zip(got, ref):
         assert abs(a - b) < tol * max(1.0, abs(b)), (got, ref)
+    if isinstance(ref, _Ref):
+        check_master_per_tensor(results[0]["master"], ref.master, ref.master0, rel=20 * tol)
+
+
+def check_master_per_tensor(got, ref, ref0, rel):
+    """Every fp32 master tensor, gathered into the single-rank layout
+    (TP shards concatenated along their split dim, ZeRO slices assembled,
+    pipeline stage names mapped to global layers), against the single-rank
+    run: ||w - w_ref|| <= rel * ||w_ref - w_init|| + 1e-3 ||w_ref|| per
+    tensor, so a permuted or misplaced shard (same norm, wrong place: error
+    ~ ||w||) fails."""
+    names = set(k.replace("#tied", "") for k in got)
+    assert names == set(ref), (sorted(names ^ set(ref)))
+    for k, w in got.items():
+        base = k.replace("#tied", "")
+        r, r0 = ref[base], ref0[base]
+        assert w.shape == r.shape, (k, w.shape, r.shape)
+        upd = float((r - r0).norm())
+        err = float((w - r).norm())
+        assert err <= rel * upd + 1e-3 * float(r.norm()), (k, err, upd)
 
 
 def test_single_process_loss_decreases(ref_losses):
@@ -263,3 +294,16 @@ def test_fused_lm_head_ce(ref_losses, layout, monkeypatch):
     loss curve."""
     monkeypatch.setenv("FLEETX_LM_HEAD_CE_CHUNK", "48")
     _check(dist_utils.run(_train, 2, layout, 3, ("Model.fused_lm_head_ce=True",)), ref_losses)
+
+
+def test_per_tensor_check_catches_a_permuted_shard():
+    """The per-tensor comparison fails on a tensor whose two TP halves were
+    concatenated in the wrong order (same values, same norm)."""
+    torch.manual_seed(0)
+    w0 = {"a": torch.randn(8, 4) * 0.02, "b": torch.zeros(8)}
+    ref = {k: v + 0.01 * torch.randn_like(v) for k, v in w0.items()}
+    check_master_per_tensor(dict(ref), ref, w0, rel=0.05)
+    bad = dict(ref)
+    bad["a"] = torch.cat([ref["a"][4:], ref["a"][:4]])
+    with pytest.raises(AssertionError):
+        check_master_per_tensor(bad, ref, w0, rel=0.05)

@@ -8,8 +8,13 @@ rounding, later steps within bf16 accumulation-order noise.
 Losses alone cannot see a gradient-scale bug (AdamW is invariant to a
 constant gradient scale), so every step also compares the pre-clip global
 gradient norm (a DP/ZeRO "sum instead of mean" doubles it) and, after the
-last step, the global norm of the fp32 master weights against the single-rank
-run.
+last step, EVERY fp32 master tensor gathered into the single-rank layout
+(``parallel/state_gather.py``: ZeRO slices assembled, TP shards concatenated
+along their split dim, pipeline stage names mapped to global layers) against
+the single-rank run -- a permuted or misplaced shard keeps every norm and
+fails here.  The DP / ZeRO layouts also run with ``FLEETX_GLOO_AS_RCCL=1``:
+the in-place reduce-scatter / all-gather-into-tensor forms the RCCL path
+issues, on device tensors.
 
 This is the device-side twin of ``tests/test_distributed_cpu.py``; RCCL itself
 is exercised by the driver's 8-GPU runs."""
@@ -61,6 +66,8 @@ def _train_gpu(rank, world, layout, steps=3, extra=()):
     g = torch.Generator().manual_seed(7)
     toks = torch.randint(0, VOCAB, (steps, GBS, SEQ + 1), generator=g)
     losses, gnorms = [], []
+    from fleetx_amd.parallel.state_gather import gather_master_state
+    master0 = gather_master_state(eng) if world == 1 else None
     for s in range(steps):
         t = toks[s, drank * local:(drank + 1) * local].cuda()
         batch = [t[:, :-1].contiguous(),
@@ -72,7 +79,8 @@ def _train_gpu(rank, world, layout, steps=3, extra=()):
     torch.cuda.synchronize()
     from fleetx_amd.ops import _lib
     return {"losses": losses, "gnorms": gnorms, "pnorm": _master_norm(eng), "drank": drank,
-            "native": _lib.kernels() is not None}
+            "native": _lib.kernels() is not None, "master": gather_master_state(eng),
+            "master0": master0}
 
 
 def _master_norm(eng):
@@ -133,6 +141,10 @@ def _check(results, ref_run):
         # fp32 master weights after the last update
         assert abs(r["pnorm"] - ref_run["pnorm"]) < 1e-3 * ref_run["pnorm"], \
             (r["pnorm"], ref_run["pnorm"])
+    # ... and tensor by tensor in the single-rank layout (bf16 compute: the
+    # per-tensor error is bounded by a fraction of the tensor's update)
+    from tests.test_distributed_cpu import check_master_per_tensor
+    check_master_per_tensor(results[0]["master"], ref_run["master"], ref_run["master0"], rel=0.1)
 
 
 LAYOUTS = {
@@ -150,6 +162,19 @@ LAYOUTS = {
 @pytest.mark.parametrize("name", sorted(LAYOUTS))
 def test_layout_matches_single_rank_on_gpu(ref_gpu, name):
     out = dist_utils.run(_train_gpu, 2, LAYOUTS[name], timeout=300)
+    _check(out, ref_gpu)
+
+
+def _train_gpu_rccl_forms(rank, world, layout):
+    os.environ["FLEETX_GLOO_AS_RCCL"] = "1"
+    return _train_gpu(rank, world, layout)
+
+
+@pytest.mark.parametrize("name", ["dp2", "zero1", "zero2", "zero3"])
+def test_rccl_collective_forms_on_gpu(ref_gpu, name):
+    """The reduce_scatter_tensor / all_gather_into_tensor calls of the RCCL
+    path (not gloo's all-reduce stand-ins) on device tensors."""
+    out = dist_utils.run(_train_gpu_rccl_forms, 2, LAYOUTS[name], timeout=300)
     _check(out, ref_gpu)
 
 
