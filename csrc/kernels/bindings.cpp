@@ -85,6 +85,8 @@ int fx_decode_gemv(int, int, int, int, int, const void*, long, const void*, long
                    const void*, long, void*, long, void*, void*, const long*, int, int, int,
                    const void*, const void*, float, hipStream_t);
 void fx_set_dropout_salt(const void*);
+hipStream_t fx_cumask_stream_create(int, int*);
+int fx_stream_destroy(hipStream_t);
 void fx_set_adamw_lr_ptr(const void*);
 int fx_comm_max_world();
 int fx_comm_max_blocks();
@@ -313,6 +315,13 @@ PYBIND11_MODULE(_kernels, m) {
                           ldy, P(kc), P(vc), reinterpret_cast<const long*>(pos), heads, head_dim,
                           maxlen, CP(ln_w), CP(ln_b), ln_eps, S(st));
   });
+  // CU-masked stream (streams.hip): returns (stream handle, CUs selected)
+  m.def("cumask_stream_create", [](int ncu) {
+    int got = 0;
+    hipStream_t s = fx_cumask_stream_create(ncu, &got);
+    return py::make_tuple(reinterpret_cast<ptr>(s), got);
+  });
+  m.def("stream_destroy", [](ptr s) { return fx_stream_destroy(S(s)); });
   // graph mode: device-resident dropout salt / AdamW learning rate (0 = off)
   m.def("set_dropout_salt", [](ptr p) { fx_set_dropout_salt(CP(p)); });
   m.def("set_adamw_lr_ptr", [](ptr p) { fx_set_adamw_lr_ptr(CP(p)); });

@@ -252,6 +252,7 @@ class EagerEngine(BasicEngine):
             if comm.get("overlap_optimizer", True) and not self._pipeline and not self._cuda_graph \
                     and hasattr(self.optimizer, "enable_forward_overlap"):
                 self.optimizer.overlap_grid = int(comm.get("overlap_optimizer_grid", 128))
+                self.optimizer.overlap_cus = int(comm.get("overlap_optimizer_cus", 0) or 0)
                 self.optimizer.enable_forward_overlap(model)
             # single data rank: gradient sum-of-squares per bucket under backward
             # (opt-in: measured neutral on 6.7B, the GEMMs leave no CU slots free)

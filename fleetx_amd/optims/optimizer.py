@@ -175,6 +175,7 @@ class FlatOptimizer:
     _overlap_groups = None
     overlap_grid = 128  # Distributed.comm.overlap_optimizer_grid
     overlap_wide = False  # Distributed.comm.overlap_optimizer_wide: 1024-thread blocks
+    overlap_cus = 0  # Distributed.comm.overlap_optimizer_cus: CU-masked stream (0 = grid cap)
 
     def enable_forward_overlap(self, model):
         """Run the parameter update of step N on a side stream, unit by unit
@@ -210,8 +211,16 @@ class FlatOptimizer:
             if cur_u is not None:
                 groups.setdefault(cur_u, []).append((ri, lo, e))
         self._overlap_groups = [(u, groups[u]) for u in sorted(groups)]  # root (-1) first
-        from ..utils.streams import side_stream
-        self._opt_stream = side_stream(buf.device)
+        from ..utils.streams import cu_masked_stream, side_stream
+        self._opt_stream = None
+        if self.overlap_cus > 0:
+            # pinned to a fixed CU set: the update may then fill those CUs
+            # (no grid cap) while every other CU runs the forward undisturbed
+            self._opt_stream = cu_masked_stream(buf.device, self.overlap_cus)
+            if self._opt_stream is not None:
+                self.overlap_grid = 0
+        if self._opt_stream is None:
+            self._opt_stream = side_stream(buf.device)
         self._unit_events = {}
         self._overlap_hooks = [model.register_forward_pre_hook(self._make_wait(-1))]
         for i, m in enumerate(units):

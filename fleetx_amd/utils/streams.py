@@ -12,7 +12,9 @@ and names them:
 * ``side``     -- ONE background stream per device shared by the
   forward-overlapped AdamW (step N's update under step N+1's forward), the
   early per-bucket gradient norm and the opt-in weight-gradient stream
-  (they never need to run concurrently with each other);
+  (they never need to run concurrently with each other); with
+  ``Distributed.comm.overlap_optimizer_cus`` the overlapped AdamW instead
+  gets a stream pinned to that many CUs (:func:`cu_masked_stream`);
 * ``copy``     -- only with ZeRO CPU offload (H2D/D2H staging);
 * one RCCL stream per process group in use.  The pipeline uses ONE
   communicator per pipe group by default: both directions of a stage link
@@ -44,6 +46,28 @@ def side_stream(device):
     return s
 
 
+_MASKED = {}
+
+
+def cu_masked_stream(device, ncu):
+    """A stream of ``device`` whose kernels run only on ``ncu`` fixed CUs
+    (``csrc/kernels/streams.hip``), as a ``torch.cuda.ExternalStream``;
+    ``None`` if the runtime refuses the mask."""
+    dev = torch.device(device)
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), int(ncu))
+    s = _MASKED.get(key)
+    if s is None:
+        from ..ops import _lib
+        with torch.cuda.device(key[0]):
+            handle, got = _lib.kernels().cumask_stream_create(int(ncu))
+        if not handle:
+            return None
+        s = torch.cuda.ExternalStream(handle, device=torch.device("cuda", key[0]))
+        s.fx_cus = got
+        _MASKED[key] = s
+    return s
+
+
 def hw_queues(env=None):
     env = os.environ if env is None else env
     try:
@@ -68,8 +92,12 @@ def inventory(hcg=None, optimizer=None, buffer=None, wgrad_stream=False):
     """``[(name, peer_waiting)]`` of the streams this rank uses."""
     out = [("compute", True)]
     side_users = []
+    masked = getattr(getattr(optimizer, "_opt_stream", None), "fx_cus", None)
     if optimizer is not None and getattr(optimizer, "_overlap_groups", None) is not None:
-        side_users.append("adamw-overlap")
+        if masked:
+            out.append(("adamw-overlap(%d CUs)" % masked, False))
+        else:
+            side_users.append("adamw-overlap")
     if buffer is not None and getattr(buffer, "_norm_stream", None) is not None:
         side_users.append("early-norm")
     if wgrad_stream:
