@@ -81,6 +81,7 @@ int fx_softmax_bwd(int, const void*, const void*, void*, long, int, int, float, 
 int fx_gemm(int, int, int, int, int, int, int, const void*, long, const void*, long, void*, long,
             const void*, void*, long, int, hipStream_t, float*, float*);
 long fx_gemm_ws_bytes(int, int, int, int);
+void fx_gemm_set_gm(int);
 int fx_decode_gemv(int, int, int, int, int, const void*, long, const void*, long, const void*,
                    const void*, long, void*, long, void*, void*, const long*, int, int, int,
                    const void*, const void*, float, hipStream_t);
@@ -306,6 +307,7 @@ PYBIND11_MODULE(_kernels, m) {
      py::arg("ldc"), py::arg("bias"), py::arg("aux"), py::arg("ldaux"), py::arg("beta"),
      py::arg("st"), py::arg("sq") = 0, py::arg("ws") = 0);
   m.def("gemm_ws_bytes", &fx_gemm_ws_bytes);
+  m.def("gemm_set_gm", &fx_gemm_set_gm);
   // decode-time skinny GEMM with fused sub-layer epilogues (decode_gemv.hip)
   m.def("decode_gemv", [](int dt, int epi, int M, int N, int K, ptr x, long ldx, ptr w, long ldw,
                           ptr bias, ptr res, long ldres, ptr y, long ldy, ptr kc, ptr vc, ptr pos,

@@ -68,6 +68,9 @@ extern "C" int fx_gemm(int dt, int la, int lb, int epi, int M, int N, int K, con
   return fx_gemm5_launch(dt, la, lb, epi, P, st);
 }
 
+// Tile-order M-group height (tools/bench_gemm.py --gm sweeps; 0 = default).
+extern "C" void fx_gemm_set_gm(int gm) { g_gm = gm > 0 ? gm : -1; }
+
 // Split-K workspace (bytes) fx_gemm wants in `ws` for an fp32 weight-gradient
 // GEMM of this shape; 0 = it runs unsplit (gemm5.hip g5_split_plan).
 extern "C" long fx_gemm_ws_bytes(int epi, int M, int N, int K) {

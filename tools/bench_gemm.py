@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--hidden", type=int, default=4096)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="", help="comma list of case names")
+    ap.add_argument("--gm", default="", help="comma list of tile-order M-group heights to A/B "
+                                             "on the hip_* cases (interleaved, one process)")
     a = ap.parse_args()
     from fleetx_amd.ops.elementwise import transpose2d
     from fleetx_amd.ops import gemm as G
@@ -80,13 +82,26 @@ def main():
             "hip_dgrad_dgelu": lambda: G.linear_dgrad(dy, w, act_input=hpre),
             "hip_wgrad_f32acc": lambda: G.linear_wgrad(dy, x, dw32, True),
         }
+        gms = [int(g) for g in a.gm.split(",")] if a.gm else [None]
+        items = []
         for k, fn in cases.items():
             if a.only and k not in a.only.split(","):
                 continue
+            if k.startswith("hip_"):
+                items += [(k if g is None else "%s_gm%d" % (k, g), fn, g) for g in gms]
+            else:
+                items.append((k, fn, None))
+        from fleetx_amd.ops import _lib
+        for k, fn, g in items:
+            if g is not None:
+                _lib.kernels().gemm_set_gm(g)
             ms = timeit(fn, a.iters)
             # TFLOP/s of the GEMM (for transposes: us per call)
             res[k] = round(ms * 1e3, 1) if k.startswith("transpose") else round(fl / ms / 1e9, 1)
         print(json.dumps(res), flush=True)
+    if a.gm:
+        from fleetx_amd.ops import _lib
+        _lib.kernels().gemm_set_gm(0)
 
 
 if __name__ == "__main__":
