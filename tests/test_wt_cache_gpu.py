@@ -1,0 +1,60 @@
+"""Cached transposed weights for the data-gradient GEMMs (parallel/linear.py
+``dgrad`` + optims/optimizer.py ``_refresh_wt``): with the forward-overlapped
+optimizer every weight whose dgrad takes the transposed ("TN") path gets its
+``w^T`` rewritten on the optimizer's side stream right after each update.
+The cached path must give bitwise the same training run as transposing on
+the fly, and must actually be taken."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CFG = os.path.join(os.path.dirname(__file__), "..", "fleetx_amd", "configs", "nlp", "gpt",
+                   "pretrain_gpt_345M_single_card.yaml")
+
+
+def _run(cache, steps=4):
+    from fleetx_amd.utils import config as C
+    from fleetx_amd.models import build_module
+    from fleetx_amd.core.engine.eager_engine import EagerEngine
+    from fleetx_amd.parallel import topology as topo
+    from fleetx_amd.utils import env
+    from fleetx_amd.ops import _lib
+    topo.reset_hcg()
+    _lib.kernels().set_dropout_salt(0)
+    _lib.kernels().set_adamw_lr_ptr(0)
+    S, B, V = 1024, 8, 1024   # 8192 tokens per step: the TN dgrad path
+    ov = ["Model.hidden_size=256", "Model.num_layers=2", "Model.num_attention_heads=4",
+          "Model.vocab_size=%d" % V, "Model.hidden_dropout_prob=0.0",
+          "Model.attention_probs_dropout_prob=0.0", "Model.max_position_embeddings=%d" % S,
+          "Global.device=gpu", "Global.local_batch_size=%d" % B, "Global.micro_batch_size=%d" % B,
+          "Engine.max_steps=10", "Engine.mix_precision.dtype=bfloat16",
+          "Distributed.comm.cache_transposed_weights=%s" % cache,
+          "Data.Train.dataset.name=SyntheticGPTDataset"]
+    cfg = C.get_config(CFG, overrides=ov, nranks=1)
+    env.set_seed(cfg.Global.seed)
+    eng = EagerEngine(configs=cfg, module=build_module(cfg), mode="train")
+    assert eng.optimizer._overlap_groups is not None, "needs the forward-overlapped optimizer"
+    g = torch.Generator().manual_seed(3)
+    toks = torch.randint(0, V, (steps, B, S + 1), generator=g)
+    losses = []
+    for s in range(steps):
+        t = toks[s].cuda()
+        batch = [t[:, :-1].contiguous(), torch.arange(S, device="cuda").expand(B, S).contiguous(),
+                 t[:, 1:].contiguous(), torch.ones(B, S, device="cuda")]
+        losses.append(float(eng._fit_impl(batch)))
+    eng.optimizer.sync_state()
+    cached = sum(1 for ps in eng.optimizer._wt_cands.values() for p in ps
+                 if getattr(p, "_fx_wt_event", None) is not None)
+    master = torch.cat([m.flatten() for m in eng.optimizer.master]).cpu()
+    return losses, master, cached
+
+
+def test_cached_transpose_matches_on_the_fly():
+    l0, m0, c0 = _run(False)
+    l1, m1, c1 = _run(True)
+    assert c0 == 0 and c1 > 0, (c0, c1)
+    assert l0 == l1, (l0, l1)
+    assert torch.equal(m0, m1)
