@@ -142,9 +142,11 @@ def _check(results, ref_run):
         assert abs(r["pnorm"] - ref_run["pnorm"]) < 1e-3 * ref_run["pnorm"], \
             (r["pnorm"], ref_run["pnorm"])
     # ... and tensor by tensor in the single-rank layout (bf16 compute: the
-    # per-tensor error is bounded by a fraction of the tensor's update)
+    # per-tensor error is bounded by a fraction of the tensor's update: 10 % seen on
+    # zero-initialised biases, where Adam turns bf16 gradient noise into sign flips;
+    # a permuted or misplaced shard gives ~140 %)
     from tests.test_distributed_cpu import check_master_per_tensor
-    check_master_per_tensor(results[0]["master"], ref_run["master"], ref_run["master0"], rel=0.1)
+    check_master_per_tensor(results[0]["master"], ref_run["master"], ref_run["master0"], rel=0.3)
 
 
 LAYOUTS = {
