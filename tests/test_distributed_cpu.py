@@ -103,7 +103,16 @@ def _check(results, ref, tol=2e-4):
         check_master_per_tensor(results[0]["master"], ref.master, ref.master0, rel=20 * tol)
 
 
-def check_master_per_tensor(got, ref, ref0, rel):
+def _drop_key_bias(t, heads):
+    """The key third of a packed [heads][3][head_dim] qkv bias, zeroed: its
+    exact gradient is 0 (a per-row constant under the softmax), so what Adam
+    makes of the rounding noise there differs between any two runs."""
+    t = t.clone()
+    t.view(heads, 3, -1)[:, 1] = 0
+    return t
+
+
+def check_master_per_tensor(got, ref, ref0, rel, heads=4):
     """Every fp32 master tensor, gathered into the single-rank layout
     (TP shards concatenated along their split dim, ZeRO slices assembled,
     pipeline stage names mapped to global layers), against the single-rank
@@ -115,6 +124,8 @@ def check_master_per_tensor(got, ref, ref0, rel):
     for k, w in got.items():
         base = k.replace("#tied", "")
         r, r0 = ref[base], ref0[base]
+        if "qkv" in base and base.endswith("bias"):
+            w, r, r0 = (_drop_key_bias(x, heads) for x in (w, r, r0))
         assert w.shape == r.shape, (k, w.shape, r.shape)
         upd = float((r - r0).norm())
         err = float((w - r).norm())
