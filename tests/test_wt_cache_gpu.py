@@ -54,7 +54,16 @@ def _run(cache, steps=4):
 
 def test_cached_transpose_matches_on_the_fly():
     l0, m0, c0 = _run(False)
+    l0b, m0b, _ = _run(False)
     l1, m1, c1 = _run(True)
     assert c0 == 0 and c1 > 0, (c0, c1)
-    assert l0 == l1, (l0, l1)
-    assert torch.equal(m0, m1)
+    det = torch.equal(m0, m0b)
+    d_rep = float((m0 - m0b).abs().max())
+    d_wt = float((m0 - m1).abs().max())
+    print("run-to-run max |dm| %.3g, cached-vs-on-the-fly %.3g, deterministic %s"
+          % (d_rep, d_wt, det))
+    if det:
+        assert l0 == l1, (l0, l1)
+        assert torch.equal(m0, m1), d_wt
+    else:  # the vendor GEMMs are not run-to-run reproducible here: same noise level
+        assert d_wt <= 4 * max(d_rep, 1e-6), (d_wt, d_rep)
