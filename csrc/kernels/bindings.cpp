@@ -82,6 +82,7 @@ int fx_gemm(int, int, int, int, int, int, int, const void*, long, const void*, l
             const void*, void*, long, int, hipStream_t, float*, float*);
 long fx_gemm_ws_bytes(int, int, int, int);
 void fx_gemm_set_gm(int);
+int fx_gemm_tuned(long*, int);
 int fx_decode_gemv(int, int, int, int, int, const void*, long, const void*, long, const void*,
                    const void*, long, void*, long, void*, void*, const long*, int, int, int,
                    const void*, const void*, float, hipStream_t);
@@ -308,6 +309,15 @@ PYBIND11_MODULE(_kernels, m) {
      py::arg("st"), py::arg("sq") = 0, py::arg("ws") = 0);
   m.def("gemm_ws_bytes", &fx_gemm_ws_bytes);
   m.def("gemm_set_gm", &fx_gemm_set_gm);
+  m.def("gemm_tuned", []() {
+    std::vector<long> buf(7 * 512);
+    const int n = fx_gemm_tuned(buf.data(), (int)buf.size());
+    py::list rows;
+    for (int i = 0; i < n; ++i)
+      rows.append(py::make_tuple(buf[7 * i], buf[7 * i + 1], buf[7 * i + 2], buf[7 * i + 3],
+                                 buf[7 * i + 4], buf[7 * i + 5], buf[7 * i + 6]));
+    return rows;
+  });
   // decode-time skinny GEMM with fused sub-layer epilogues (decode_gemv.hip)
   m.def("decode_gemv", [](int dt, int epi, int M, int N, int K, ptr x, long ldx, ptr w, long ldw,
                           ptr bias, ptr res, long ldres, ptr y, long ldy, ptr kc, ptr vc, ptr pos,

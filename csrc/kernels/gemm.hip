@@ -21,6 +21,10 @@
 // live in tools/gemm_lab/gemm_legacy.hip for lab A/Bs only.
 #include <stdlib.h>
 
+#include <map>
+#include <tuple>
+#include <vector>
+
 #include "fx_common.h"
 #include "gemm_common.h"
 
@@ -29,7 +33,67 @@ long fx_gemm5_ws_bytes(int M, int N, int K);
 
 using namespace fxg;
 
-static int g_gm = -1;  // FLEETX_GEMM_GM: M-group height of the tile order (default 8)
+static int g_gm = -1;  // FLEETX_GEMM_GM / fx_gemm_set_gm: force the tile-order M-group height
+
+// Tile-order autotune (FLEETX_GEMM_TUNE, default on).  The M-group height
+// `gm` of the tile order decides which A / B panels the 32 concurrent
+// workgroups of an XCD share; the best value depends on the shape and the
+// operand layouts (GPT-3 6.7B, one box: weight gradient of the QKV
+// projection 1206 TF/s at gm 8 vs 1306 at gm 4, data gradient of FC1 1378 vs
+// 1514 at gm 2, forward of QKV 1419 vs 1466 at gm 2; profiles/r4_gm/).  On a
+// shape's first call outside stream capture, every candidate runs into a
+// scratch output (fp32 / 16-bit store epilogue, beta 0, no norm partials)
+// and the fastest is cached per (layouts, fp32 output, M, N, K).  The tile
+// order never changes a tile's arithmetic: results are bitwise identical for
+// every gm.
+static int g_tune = -1;
+static std::map<std::tuple<int, int, int, int, int, int>, int> g_gm_tuned;
+static const int kGmCand[] = {1, 2, 4, 8, 16};
+
+static int gemm_tuned_gm(int dt, int la, int lb, int epi, const GemmParams& P0, hipStream_t st) {
+  const int f32 = epi == EPI_F32;
+  const auto key = std::make_tuple(la, lb, f32, P0.M, P0.N, P0.K);
+  auto it = g_gm_tuned.find(key);
+  if (it != g_gm_tuned.end()) return it->second;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return 8;
+  void* scratch = nullptr;
+  if (hipMalloc(&scratch, (size_t)P0.M * P0.N * (f32 ? 4 : 2)) != hipSuccess) {
+    (void)hipGetLastError();
+    return 8;
+  }
+  GemmParams P = P0;
+  P.C = scratch;
+  P.ldc = P0.N;
+  P.bias = nullptr;
+  P.aux = nullptr;
+  P.beta = 0;
+  P.sq = nullptr;
+  const int tepi = f32 ? EPI_F32 : EPI_STORE;
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  int best = 8;
+  float bt = 1e30f;
+  for (int gm : kGmCand) {
+    P.gm = gm;
+    if (fx_gemm5_launch(dt, la, lb, tepi, P, st) != 0) break;
+    (void)hipEventRecord(e0, st);
+    for (int r = 0; r < 3; ++r) (void)fx_gemm5_launch(dt, la, lb, tepi, P, st);
+    (void)hipEventRecord(e1, st);
+    (void)hipEventSynchronize(e1);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms < bt) {
+      bt = ms;
+      best = gm;
+    }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(scratch);
+  g_gm_tuned[key] = best;
+  return best;
+}
 
 // Returns 0 when launched, < 0 when the shape / layout / epilogue is not
 // covered (the caller falls back to hipBLASLt):
@@ -58,18 +122,35 @@ extern "C" int fx_gemm(int dt, int la, int lb, int epi, int M, int N, int K, con
   P.lda = lda; P.ldb = ldb; P.ldc = ldc; P.ldaux = ldaux;
   P.M = M; P.N = N; P.K = K;
   P.beta = beta;
-  if (g_gm < 0) {
-    const char* e = getenv("FLEETX_GEMM_GM");
-    g_gm = e ? atoi(e) : 8;
-  }
-  P.gm = g_gm > 0 ? g_gm : 8;
   P.sq = sq;
   P.ws = epi == EPI_F32 ? ws : nullptr;
+  if (g_gm < 0) {
+    const char* e = getenv("FLEETX_GEMM_GM");
+    g_gm = e ? atoi(e) : 0;
+  }
+  if (g_tune < 0) {
+    const char* e = getenv("FLEETX_GEMM_TUNE");
+    g_tune = e ? atoi(e) : 1;
+  }
+  P.gm = g_gm > 0 ? g_gm : (g_tune ? gemm_tuned_gm(dt, la, lb, epi, P, st) : 8);
   return fx_gemm5_launch(dt, la, lb, epi, P, st);
 }
 
-// Tile-order M-group height (tools/bench_gemm.py --gm sweeps; 0 = default).
-extern "C" void fx_gemm_set_gm(int gm) { g_gm = gm > 0 ? gm : -1; }
+// Tile-order M-group height (tools/bench_gemm.py --gm sweeps; 0 = tuned / default).
+extern "C" void fx_gemm_set_gm(int gm) { g_gm = gm > 0 ? gm : 0; }
+
+// The tuned table: (la, lb, fp32 out, M, N, K, gm) rows, flattened.
+extern "C" int fx_gemm_tuned(long* out, int cap) {
+  int n = 0;
+  for (const auto& kv : g_gm_tuned) {
+    if (n + 7 > cap) break;
+    out[n++] = std::get<0>(kv.first); out[n++] = std::get<1>(kv.first);
+    out[n++] = std::get<2>(kv.first); out[n++] = std::get<3>(kv.first);
+    out[n++] = std::get<4>(kv.first); out[n++] = std::get<5>(kv.first);
+    out[n++] = kv.second;
+  }
+  return n / 7;
+}
 
 // Split-K workspace (bytes) fx_gemm wants in `ws` for an fp32 weight-gradient
 // GEMM of this shape; 0 = it runs unsplit (gemm5.hip g5_split_plan).

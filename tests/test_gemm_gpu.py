@@ -214,3 +214,29 @@ def test_persistent_many_tiles(gemm, K):
     base = out.clone()
     assert gemm.linear_wgrad(dy, x, out, True)
     assert _rel(out, dy.float().t() @ x.float() + base) < 1e-4
+
+
+def test_tile_order_autotune_is_bitwise_neutral(gemm):
+    """The tuned tile-order M-group (csrc/kernels/gemm.hip gemm_tuned_gm)
+    changes only which workgroup computes which tile: outputs are bitwise
+    those of the default order, and the shape lands in the tuned table."""
+    from fleetx_amd.ops import _lib
+    k = _lib.kernels()
+    torch.manual_seed(11)
+    M, N, K = 4096, 3072, 1024
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    outs = []
+    for gm in (8, 0, 1):          # forced default, tuned, forced 1
+        k.gemm_set_gm(gm)
+        o32 = torch.zeros(N, K, device="cuda", dtype=torch.float32)
+        assert gemm.linear_wgrad(dy, x, o32, False)
+        outs.append((gemm.linear_fwd(x, w), gemm.linear_dgrad(dy, w), o32))
+    k.gemm_set_gm(0)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    for a, b in zip(outs[0], outs[2]):
+        assert torch.equal(a, b)
+    tuned = {(r[0], r[1], r[2], r[3], r[4], r[5]): r[6] for r in k.gemm_tuned()}
+    assert (1, 1, 1, N, K, M) in tuned and tuned[(1, 1, 1, N, K, M)] in (1, 2, 4, 8, 16)
