@@ -253,7 +253,6 @@ class EagerEngine(BasicEngine):
                     and hasattr(self.optimizer, "enable_forward_overlap"):
                 self.optimizer.overlap_grid = int(comm.get("overlap_optimizer_grid", 128))
                 self.optimizer.overlap_cus = int(comm.get("overlap_optimizer_cus", 0) or 0)
-                self.optimizer.cache_wt = bool(comm.get("cache_transposed_weights", True))
                 self.optimizer.enable_forward_overlap(model)
             # single data rank: gradient sum-of-squares per bucket under backward
             # (opt-in: measured neutral on 6.7B, the GEMMs leave no CU slots free)
@@ -698,8 +697,6 @@ class EagerEngine(BasicEngine):
         if not os.path.isfile(mp):
             raise FileNotFoundError("{} not found".format(mp))
         sd = ckpt.load_payload(mp)
-        if hasattr(self.optimizer, "drop_wt_cache"):
-            self.optimizer.drop_wt_cache()   # parameters rewritten below
         with self._params_gathered(writeback=True):
             res = self._module.model.load_state_dict(sd, strict=False)
         missing = [k for k in res.missing_keys

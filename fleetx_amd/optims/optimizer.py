@@ -176,7 +176,6 @@ class FlatOptimizer:
     overlap_grid = 128  # Distributed.comm.overlap_optimizer_grid
     overlap_wide = False  # Distributed.comm.overlap_optimizer_wide: 1024-thread blocks
     overlap_cus = 0  # Distributed.comm.overlap_optimizer_cus: CU-masked stream (0 = grid cap)
-    cache_wt = True  # Distributed.comm.cache_transposed_weights: w^T for dgrad, see _refresh_wt
 
     def enable_forward_overlap(self, model):
         """Run the parameter update of step N on a side stream, unit by unit
@@ -212,11 +211,6 @@ class FlatOptimizer:
             if cur_u is not None:
                 groups.setdefault(cur_u, []).append((ri, lo, e))
         self._overlap_groups = [(u, groups[u]) for u in sorted(groups)]  # root (-1) first
-        # 2-D weights per unit that may want a cached transpose (parallel/linear.py dgrad)
-        self._wt_cands = {}
-        for n, p in buf.params:
-            if getattr(p, "_fx_cache_wt_ok", False) and p.dim() == 2:
-                self._wt_cands.setdefault(owner.get(id(p), -1), []).append(p)
         from ..utils.streams import cu_masked_stream, side_stream
         self._opt_stream = None
         if self.overlap_cus > 0:
@@ -262,7 +256,6 @@ class FlatOptimizer:
 
     def refresh_master_from_params(self):
         self.sync_state()
-        self.drop_wt_cache()
         for (s, e, _), m in zip(self.ranges, self.master):
             m.copy_(self.buffer.param_flat[s:e].float())
 
@@ -356,37 +349,8 @@ class FusedAdamW(FlatOptimizer):
                 ev = torch.cuda.Event()
                 ev.record(os_)
                 self._unit_events[u] = ev
-                if self.cache_wt:
-                    self._refresh_wt(u)
         if grid:
             k.adamw_tune(0, 1, 0)
-
-    def _refresh_wt(self, unit):
-        """Rewrite the cached ``w^T`` of this unit's weights whose data
-        gradient asked for one (``_fx_wt_wanted``, set by the first backward
-        that transposed on the fly) on the side stream, right behind the
-        unit's update: the LDS transpose then runs beside the next forward's
-        GEMMs, and the backward's dgrad waits only for its own weight's
-        event.  Stale caches never survive: every path that rewrites
-        parameters outside this one drops them (``drop_wt_cache``)."""
-        from ..ops.elementwise import transpose2d
-        for p in self._wt_cands.get(unit, ()):
-            if not getattr(p, "_fx_wt_wanted", False):
-                continue
-            wt = getattr(p, "_fx_wt", None)
-            if wt is None:
-                wt = p._fx_wt = torch.empty(p.shape[1], p.shape[0], dtype=p.dtype,
-                                            device=p.device)
-            transpose2d(p.data, out=wt)
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream())
-            p._fx_wt_event = ev
-
-    def drop_wt_cache(self):
-        """Forget every cached ``w^T`` (parameters changed elsewhere)."""
-        for ps in getattr(self, "_wt_cands", {}).values():
-            for p in ps:
-                p._fx_wt_event = None
 
     def _update_offloaded(self, lr):
         """Stream host-resident master/m/v through the GPU in chunks: the H2D
@@ -441,7 +405,6 @@ class FusedAdamW(FlatOptimizer):
             return self._update_offloaded(lr)
         if self._overlap_groups is not None and self.decoupled:
             return self._update_overlapped(lr)
-        self.drop_wt_cache()
         pf = self.buffer.param_flat
         for (s, e, c), g, p, m, v in zip(self.ranges, self.grad_views(), self.master, self.m,
                                          self.v):
@@ -480,7 +443,6 @@ class FusedAdamW(FlatOptimizer):
 
     def set_state_dict(self, state):
         self.sync_state()
-        self.drop_wt_cache()
         self.step_count = state["step"]
         self.dev_step.fill_(int(state.get("applied_step", state["step"])))
         for dst, src in zip(self.master, state["master"]):

@@ -97,7 +97,6 @@ class ColumnParallelLinear(nn.Module):
                                                         device=device))
         self.weight.tp_split = t > 1
         self.weight.tp_dim = 0
-        self.weight._fx_cache_wt_ok = True  # dgrad may use an optimizer-cached w^T
         self.weight._fx_fused_wgrad_ok = True
         self.weight._fx_gemm_wgrad = True  # gradient from the wgrad GEMM (fused-norm partials)
         if bias:
@@ -149,7 +148,6 @@ class RowParallelLinear(nn.Module):
                                                         device=device))
         self.weight.tp_split = t > 1
         self.weight.tp_dim = 1
-        self.weight._fx_cache_wt_ok = True
         self.weight._fx_fused_wgrad_ok = True
         self.weight._fx_gemm_wgrad = True  # gradient from the wgrad GEMM (fused-norm partials)
         if bias:
@@ -195,7 +193,6 @@ class VocabParallelEmbedding(nn.Module):
                                                         dim=0, dtype=dtype, device=device))
         self.weight.tp_split = t > 1
         self.weight.tp_dim = 0
-        self.weight._fx_cache_wt_ok = True  # the tied LM head's dgrad
 
     def forward(self, ids, pos_ids=None, pos_weight=None, reduce=True):
         out = ops.embedding(ids, self.weight, pos_ids, pos_weight, self.vocab_start)

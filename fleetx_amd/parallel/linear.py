@@ -49,21 +49,12 @@ def dgrad(dy, w):
     The transpose costs ~4 B per weight element at ~4.5 TB/s while the GEMM
     saves ~13 % of 2*M FLOPs per element at ~1.4 PFLOP/s: it pays off from
     M ~ 4.5k rows, so smaller micro-batches (pipeline schedules) keep NN.
-
-    Under the forward-overlapped optimizer the transpose is not done here at
-    all: a weight that took this path asks for a cached ``w^T``
-    (``_fx_wt_wanted``), which the optimizer rewrites on its side stream
-    right after each update (``FlatOptimizer._refresh_wt``) -- beside the
-    next forward's GEMMs instead of inside the backward."""
+    (Caching ``w^T`` -- rewritten by the forward-overlapped optimizer beside
+    the next forward -- measured 4.7 ms/step SLOWER on 6.7B than transposing
+    here: that region is already bandwidth-saturated; profiles/r4_step/.)"""
     if dy.is_cuda and dy.dtype in (torch.bfloat16, torch.float16) \
             and w.dtype == dy.dtype and w.dim() == 2 and w.shape[0] % 8 == 0 \
             and w.shape[1] % 8 == 0 and dy.numel() // dy.shape[-1] >= 6144:
-        ev = getattr(w, "_fx_wt_event", None)
-        if ev is not None:
-            torch.cuda.current_stream().wait_event(ev)
-            return F.linear(dy, w._fx_wt)
-        if getattr(w, "_fx_cache_wt_ok", False):
-            w._fx_wt_wanted = True
         from ..ops.elementwise import transpose2d
         return F.linear(dy, transpose2d(w))
     return torch.matmul(dy, w)
