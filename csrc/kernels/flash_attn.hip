@@ -235,10 +235,7 @@ struct AttnParams {
   uint32_t klo, khi, thr;
   float drop_scale;
   int dval;              // valid head dim (<= the tile's D; columns past it are zero)
-  int delta_in_dq;       // backward: the dQ pass computes and stores delta (no pre-pass)
   const uint64_t* salt;  // graph mode: per-replay device salt (fx_set_dropout_salt)
-  int full_tiles;        // forward: compute fully masked key halves too (A/B, FLEETX_FA_HALF_SKIP=0)
-  int dq_half_skip;      // dQ: skip fully masked key halves (FLEETX_FA_DQ_HALF_SKIP=0 turns it off)
 };
 
 // per-(batch, head) dropout hash seed; under graph mode the baked key is
@@ -310,7 +307,7 @@ __device__ __forceinline__ void fwd_tile(const AttnParams& P, const Frag<D>& F, 
     // the tile's second 32-key half is skipped (scores -inf, no MFMAs) when
     // every key in it is past kv_len (the tail tile of S = 257) or above the
     // causal diagonal of all this wave's queries (wave-uniform)
-    const bool half2 = P.full_tiles || (kb + 32 < kv_len && !(CAUSAL && kb + 32 > wq0 + 31));
+    const bool half2 = (kb + 32 < kv_len && !(CAUSAL && kb + 32 > wq0 + 31));
     // all K fragments of the tile up front: the 16 LDS reads overlap each
     // other instead of one exposed LDS latency per MFMA
     short8 kfr[2][D / 16];
@@ -512,34 +509,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
 }
 
 // ============================================================================
-// backward preprocess: delta[bh, q] = sum_d dO * O
-// ============================================================================
-template <typename T, int D>
-__global__ __launch_bounds__(256) void fa_bwd_pre_kernel(AttnParams P) {
-  // 8 elements (16 B) per thread; TPR = D/8 rounded up to a power of two
-  // threads per row (the extra threads of D = 96 contribute 0)
-  constexpr int TPR = D / 8 <= 8 ? 8 : 16;
-  const long row = (long)blockIdx.x * (256 / TPR) + threadIdx.x / TPR;
-  const int c = (threadIdx.x % TPR) * 8;
-  const long total = (long)P.B * P.H * P.Sq;
-  float s = 0.f;
-  if (row < total && c < P.dval) {
-    const int q = row % P.Sq;
-    const int bh = row / P.Sq;
-    const int b = bh / P.H, hd = bh % P.H;
-    const long off = b * P.so_b + hd * P.so_h + (long)q * P.so_s + c;
-    float a[8], g[8];
-    load8<T>(P.o + off, a);
-    load8<T>(P.dout + off, g);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s += a[j] * g[j];
-  }
-#pragma unroll
-  for (int o = TPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  if (row < total && (threadIdx.x % TPR) == 0) P.delta[row] = s;
-}
-
-// ============================================================================
 // backward dQ: WG = 4 waves x 32 queries; loop over 64-key tiles.
 //   S^T = K.Q^T, dP^T = V.dO^T (queries on lanes), dQ^T += K^T.dS^T
 // ============================================================================
@@ -607,9 +576,9 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
     vld.load(0, smem + 2 * TB, lane);
   }
   // delta = rowsum(dO . O): taken here from the dO fragments already in
-  // registers plus one load of the O row (in flight with the first K/V tile) (the dK/dV pass, launched after this
-  // one, reads the stored value), or from the separate pre-pass
-  if (P.delta_in_dq) {
+  // registers plus one load of the O row (in flight with the first K/V tile);
+  // the dK/dV pass, launched after this one, reads the stored value
+  {
     float part = 0.f;
     if (qvalid) {
       const uint16_t* orow = P.o + b * P.so_b + hd * P.so_h + (long)qi * P.so_s;
@@ -626,8 +595,6 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
     part += __shfl_xor(part, 32, 64);
     dlt = qvalid ? part : 0.f;
     if (qvalid && h == 0) P.delta[(long)bh * P.Sq + qi] = dlt;
-  } else {
-    dlt = qvalid ? P.delta[(long)bh * P.Sq + qi] : 0.f;
   }
   glds_wait();
   __syncthreads();
@@ -647,8 +614,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
       const bool need_mask = (CAUSAL && kb + KV - 1 > wq0) || (kb + KV > kv_len);
       // second 32-key half fully masked (P = 0 there, so dS = 0): skipped as in
       // the forward (ViT-g backward 291.8 -> 280.0 us, causal D 64 / 128
-      // neutral: profiles/r3_fahalf/; FLEETX_FA_DQ_HALF_SKIP=0 for A/B)
-      const bool half2 = !P.dq_half_skip || (kb + 32 < kv_len && !(CAUSAL && kb + 32 > wq0 + 31));
+      // neutral: profiles/r3_fahalf/)
+      const bool half2 = (kb + 32 < kv_len && !(CAUSAL && kb + 32 > wq0 + 31));
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         if (t == 1 && !half2) continue;
@@ -978,10 +945,6 @@ AttnParams make_params(const void* q, const void* k, const void* v, const long* 
   P.khi = (uint32_t)(key >> 32);
   P.thr = (uint32_t)(p * 65536.0f + 0.5f);
   P.drop_scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
-  static const int half_skip = [] { const char* e = getenv("FLEETX_FA_HALF_SKIP"); return e ? atoi(e) : 1; }();
-  P.full_tiles = !half_skip;
-  static const int dq_skip = [] { const char* e = getenv("FLEETX_FA_DQ_HALF_SKIP"); return e ? atoi(e) : 1; }();
-  P.dq_half_skip = dq_skip;
   P.salt = p > 0.f ? g_fx_dropout_salt : nullptr;
   return P;
 }
@@ -1114,19 +1077,6 @@ static int flash_bwd_t(const void* q, const void* k, const void* v, const void* 
   P.so_b = os[0]; P.so_s = os[1]; P.so_h = os[2];
   P.sdk_b = dks[0]; P.sdk_s = dks[1]; P.sdk_h = dks[2];
   P.sdq_b = dqs[0]; P.sdq_s = dqs[1]; P.sdq_h = dqs[2];
-  static const bool delta_fused = [] {
-    const char* e = getenv("FLEETX_FA_DELTA_IN_DQ");
-    return e == nullptr || atoi(e) != 0;
-  }();
-  P.delta_in_dq = delta_fused ? 1 : 0;
-  if (!delta_fused) {
-    const long rows = (long)B * H * Sq;
-    const int rpb = 256 / (D / 8 <= 8 ? 8 : 16);  // rows per block (fa_bwd_pre_kernel TPR)
-    const int grid = (int)((rows + rpb - 1) / rpb);
-    if (D == 128) fa_bwd_pre_kernel<T, 128><<<grid, 256, 0, st>>>(P);
-    else if (D == 96) fa_bwd_pre_kernel<T, 96><<<grid, 256, 0, st>>>(P);
-    else fa_bwd_pre_kernel<T, 64><<<grid, 256, 0, st>>>(P);
-  }
   {
     const int nq = (Sq + 127) / 128;
     const size_t smem = 4 * 64 * D * 2;
@@ -1137,9 +1087,7 @@ static int flash_bwd_t(const void* q, const void* k, const void* v, const void* 
     // double-buffered Q/dO tiles + row constants, then the WG's V rows
     // D <= 96: 64-query tiles with V in registers (bwd 0.150 -> 0.144 ms at
     // B8 S1024 H16 D64, profiles/r3_dkdv/); D = 128 has no 32 VGPRs to spare.
-    // FLEETX_FA_DKDV=32 keeps 32-query tiles everywhere (A/B switch).
-    const char* e = getenv("FLEETX_FA_DKDV");
-    if (D <= 96 && (e == nullptr || atoi(e) != 32)) {
+    if (D <= 96) {
       const size_t smem = 2 * (2 * 64 * D * 2 + 2 * 64 * 4);
       FA_DISPATCH(fa_bwd_dkdv_q64v_kernel, D, causal, p > 0.f, kbias != nullptr, nk * B * H,
                   smem, st, P);

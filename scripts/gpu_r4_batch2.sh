@@ -4,7 +4,7 @@ set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r4b2
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gemm_gpu.py tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit 1
 run() {  # tag, env
   env $2 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > $O/$1.log 2>&1 || { tail -5 $O/$1.log; exit 1; }
