@@ -82,6 +82,7 @@ int fx_gemm(int, int, int, int, int, int, int, const void*, long, const void*, l
             const void*, void*, long, int, hipStream_t, float*, float*);
 long fx_gemm_ws_bytes(int, int, int, int);
 void fx_gemm_set_gm(int);
+void fx_gemm_set_geom(int, int);
 int fx_gemm_tuned(long*, int);
 int fx_decode_gemv(int, int, int, int, int, const void*, long, const void*, long, const void*,
                    const void*, long, void*, long, void*, void*, const long*, int, int, int,
@@ -309,6 +310,7 @@ PYBIND11_MODULE(_kernels, m) {
      py::arg("st"), py::arg("sq") = 0, py::arg("ws") = 0);
   m.def("gemm_ws_bytes", &fx_gemm_ws_bytes);
   m.def("gemm_set_gm", &fx_gemm_set_gm);
+  m.def("gemm_set_geom", &fx_gemm_set_geom);
   m.def("gemm_tuned", []() {
     std::vector<long> buf(7 * 512);
     const int n = fx_gemm_tuned(buf.data(), (int)buf.size());

@@ -30,6 +30,7 @@
 
 int fx_gemm5_launch(int dt, int la, int lb, int epi, const fxg::GemmParams& P, hipStream_t st);
 long fx_gemm5_ws_bytes(int M, int N, int K);
+void fx_gemm5_set_geom(int nf, int split);
 
 using namespace fxg;
 
@@ -138,6 +139,10 @@ extern "C" int fx_gemm(int dt, int la, int lb, int epi, int M, int N, int K, con
 
 // Tile-order M-group height (tools/bench_gemm.py --gm sweeps; 0 = tuned / default).
 extern "C" void fx_gemm_set_gm(int gm) { g_gm = gm > 0 ? gm : 0; }
+
+// Lab override of the tile geometry (4 / 8) and split-K slices (1 = none);
+// 0 = the shape's plan.
+extern "C" void fx_gemm_set_geom(int nf, int split) { fx_gemm5_set_geom(nf, split); }
 
 // The tuned table: (la, lb, fp32 out, M, N, K, gm) rows, flattened.
 extern "C" int fx_gemm_tuned(long* out, int cap) {

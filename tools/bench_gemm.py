@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--tokens", type=int, default=8192)
     ap.add_argument("--hidden", type=int, default=4096)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--geom", default="", help="comma list of nf:split lab geometries for the "
+                                               "hip_wgrad cases, e.g. 4:1,4:2,8:4 (0:0 = plan)")
+    ap.add_argument("--vocab", type=int, default=0, help="also time the LM head (h -> vocab)")
     ap.add_argument("--only", default="", help="comma list of case names")
     ap.add_argument("--gm", default="", help="comma list of tile-order M-group heights to A/B "
                                              "on the hip_* cases (interleaved, one process)")
@@ -41,6 +44,8 @@ def main():
     M, h = a.tokens, a.hidden
     dev, bf = "cuda", torch.bfloat16
     shapes = {"qkv": (h, 3 * h), "out": (h, h), "fc1": (h, 4 * h), "fc2": (4 * h, h)}
+    if a.vocab:
+        shapes["head"] = (h, a.vocab)
     for name, (K, N) in shapes.items():
         x = torch.randn(M, K, device=dev, dtype=bf)
         w = torch.randn(N, K, device=dev, dtype=bf) * 0.02       # [out, in]
@@ -83,25 +88,31 @@ def main():
             "hip_wgrad_f32acc": lambda: G.linear_wgrad(dy, x, dw32, True),
         }
         gms = [int(g) for g in a.gm.split(",")] if a.gm else [None]
+        geoms = [tuple(int(v) for v in g.split(":")) for g in a.geom.split(",")] if a.geom else [None]
         items = []
         for k, fn in cases.items():
             if a.only and k not in a.only.split(","):
                 continue
-            if k.startswith("hip_"):
-                items += [(k if g is None else "%s_gm%d" % (k, g), fn, g) for g in gms]
+            if k.startswith("hip_wgrad"):
+                items += [(k + ("" if g is None else "_gm%d" % g) +
+                           ("" if q is None else "_g%d:%d" % q), fn, g, q) for g in gms for q in geoms]
+            elif k.startswith("hip_"):
+                items += [(k if g is None else "%s_gm%d" % (k, g), fn, g, None) for g in gms]
             else:
-                items.append((k, fn, None))
+                items.append((k, fn, None, None))
         from fleetx_amd.ops import _lib
-        for k, fn, g in items:
+        for k, fn, g, q in items:
             if g is not None:
                 _lib.kernels().gemm_set_gm(g)
+            _lib.kernels().gemm_set_geom(*(q or (0, 0)))
             ms = timeit(fn, a.iters)
             # TFLOP/s of the GEMM (for transposes: us per call)
             res[k] = round(ms * 1e3, 1) if k.startswith("transpose") else round(fl / ms / 1e9, 1)
         print(json.dumps(res), flush=True)
-    if a.gm:
+    if a.gm or a.geom:
         from fleetx_amd.ops import _lib
         _lib.kernels().gemm_set_gm(0)
+        _lib.kernels().gemm_set_geom(0, 0)
 
 
 if __name__ == "__main__":
