@@ -104,6 +104,69 @@ def out_tiles(kind, a, b, t=128):
     return _tiles(a.shape[-1], b.shape[-1], t)
 
 
+# Per-shape routing of the plain forward / data-gradient GEMMs
+# (FLEETX_GEMM_ROUTE=tune, the default; "off" keeps the kind table alone).
+# Which of the MFMA kernel and hipBLASLt is faster depends on the shape
+# (GPT-3 6.7B with the tuned tile order: QKV forward 1466 vs 1331 TF/s, FC1
+# forward 1414 vs 1521; data gradients of QKV / out / FC1 lead, FC2 trails;
+# profiles/r4_gm/).  The first call of a (kind, shape) outside stream capture
+# times both paths (interleaved, a few launches each, on the caller's
+# stream) and the kernel takes the shape only when it wins by ROUTE_MARGIN,
+# so near-ties stay on one side from run to run.  The vendor path of a kind
+# is registered by its caller (VENDOR).
+ROUTE_TUNE = os.environ.get("FLEETX_GEMM_ROUTE", "tune") == "tune"
+TUNE_KINDS = ("fwd", "dgrad")
+ROUTE_MARGIN = 0.03
+VENDOR = {}
+_ROUTE = {}
+
+
+def route_table():
+    """{(kind, M, N, K): True if the MFMA kernel takes it} decided so far."""
+    return {k[:4]: v for k, v in _ROUTE.items()}
+
+
+def _race(f_hip, f_vendor, iters=3):
+    if f_hip() is None:
+        return False
+    f_vendor()
+    t = []
+    for f in (f_hip, f_vendor, f_hip, f_vendor):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            f()
+        e1.record()
+        e1.synchronize()
+        t.append(e0.elapsed_time(e1))
+    return min(t[0], t[2]) < (1.0 - ROUTE_MARGIN) * min(t[1], t[3])
+
+
+def _tuned_route(kind, a, b):
+    a2 = a.reshape(-1, a.shape[-1])
+    M = a2.shape[0]
+    if kind == "fwd":
+        N, K = b.shape[0], b.shape[1]
+    else:
+        N, K = b.shape[1], b.shape[0]
+    key = (kind, M, N, K, a.dtype)
+    r = _ROUTE.get(key)
+    if r is not None:
+        return r
+    if out_tiles(kind, a, b) < MIN_TILES or kind not in VENDOR or not _ok(a2, b):
+        _ROUTE[key] = False
+        return False
+    if torch.cuda.is_current_stream_capturing():
+        return False
+    if kind == "fwd":
+        r = _race(lambda: linear_fwd(a2, b), lambda: VENDOR["fwd"](a2, b))
+    else:
+        r = _race(lambda: linear_dgrad(a2, b), lambda: VENDOR["dgrad"](a2, b))
+    _ROUTE[key] = r
+    return r
+
+
 def use(kind, a, b=None):
     """Whether GEMM ``kind`` ('fwd' | 'fwd_act' | 'dgrad' | 'dgrad_act' |
     'wgrad'; ``_act`` = with the GeLU / GeLU' epilogue) on these operands goes
@@ -111,9 +174,13 @@ def use(kind, a, b=None):
     if _MODE == "blas" or not a.is_cuda or a.dtype not in (torch.bfloat16, torch.float16):
         return False
     if _MODE == "auto":
-        if kind not in AUTO_KINDS or b is None:
+        if b is None:
             return False
-        return out_tiles(kind, a, b) >= (WGRAD_MIN_TILES if kind == "wgrad" else MIN_TILES)
+        if kind in AUTO_KINDS:
+            return out_tiles(kind, a, b) >= (WGRAD_MIN_TILES if kind == "wgrad" else MIN_TILES)
+        if ROUTE_TUNE and kind in TUNE_KINDS:
+            return _tuned_route(kind, a, b)
+        return False
     return True
 
 

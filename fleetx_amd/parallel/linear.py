@@ -60,6 +60,10 @@ def dgrad(dy, w):
     return torch.matmul(dy, w)
 
 
+G.VENDOR["dgrad"] = dgrad
+G.VENDOR["fwd"] = F.linear
+
+
 def _fused(p):
     return p is not None and getattr(p, "_fx_fused_wgrad", False) and hasattr(p, "main_grad")
 

@@ -240,3 +240,55 @@ def test_tile_order_autotune_is_bitwise_neutral(gemm):
         assert torch.equal(a, b)
     tuned = {(r[0], r[1], r[2], r[3], r[4], r[5]): r[6] for r in k.gemm_tuned()}
     assert (1, 1, 1, N, K, M) in tuned and tuned[(1, 1, 1, N, K, M)] in (1, 2, 4, 8, 16)
+
+
+def test_route_tuner_picks_a_path_and_both_agree():
+    """Per-shape routing of plain forward / data-gradient GEMMs (ops/gemm.py
+    _tuned_route): the first call of a shape races the MFMA kernel against the
+    registered vendor path, caches the winner, and either path matches fp32."""
+    from fleetx_amd.ops import gemm as G
+    from fleetx_amd.parallel import linear as L
+    old = (G._MODE, G.ROUTE_TUNE, set(G.AUTO_KINDS))
+    try:
+        G.set_mode("auto")
+        G.ROUTE_TUNE = True
+        G.set_auto_kinds("wgrad")
+        torch.manual_seed(12)
+        M, N, K = 4096, 6144, 1024
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+        dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+        y = L.fwd_gemm(x, w)
+        dx = L.dgrad_gemm(dy, w)
+        table = G.route_table()
+        assert ("fwd", M, N, K) in table and ("dgrad", M, K, N) in table
+        assert _rel(y, x.float() @ w.float().t()) < 1e-2
+        assert _rel(dx, dy.float() @ w.float()) < 1e-2
+        # small outputs never race (under MIN_TILES): vendor path, cached False
+        xs = torch.randn(256, K, device="cuda", dtype=torch.bfloat16)
+        L.fwd_gemm(xs, w[:512])
+        assert G.route_table()[("fwd", 256, 512, K)] is False
+    finally:
+        G.set_mode(old[0])
+        G.ROUTE_TUNE = old[1]
+        G.set_auto_kinds(old[2])
+
+
+@pytest.mark.parametrize("nf,split", [(4, 1), (4, 3), (8, 2), (8, 1)])
+def test_wgrad_forced_geometry(gemm, nf, split):
+    """The lab geometry / split-K override (fx_gemm_set_geom) used by
+    tools/bench_gemm.py --geom: every forced plan computes the same product."""
+    from fleetx_amd.ops import _lib
+    k = _lib.kernels()
+    torch.manual_seed(13)
+    M, N, K = 2048, 1024, 768
+    dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    base = torch.randn(N, K, device="cuda", dtype=torch.float32)
+    try:
+        k.gemm_set_geom(nf, split)
+        out = base.clone()
+        assert gemm.linear_wgrad(dy, x, out, True)
+    finally:
+        k.gemm_set_geom(0, 0)
+    assert _rel(out, base + dy.float().t() @ x.float()) < 1e-4
