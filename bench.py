@@ -202,6 +202,7 @@ def main():
         else "", "tp%d" % mp if mp > 1 else "", "pp%d" % pp if pp > 1 else "",
         "sp" if args.sequence_parallel and mp > 1 else "") if x) or "dp1"
     if env.get_rank() == 0:
+        from fleetx_amd.ops import gemm as gemm_routes
         out = {
             "metric": "tokens/sec (whole node) GPT-3 6.7B hybrid-parallel at 1/2/4/8 MI355X"
             if args.model == "gpt3-6.7B" else "tokens/sec %s" % args.model,
@@ -229,6 +230,9 @@ def main():
             "final_loss": round(lval, 4),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)
             if torch.cuda.is_available() else None,
+            # shapes the per-shape GEMM race sent to the MFMA kernel (ops/gemm.py)
+            "gemm_raced_to_kernel": sorted("%s %dx%dx%d" % k for k, v in
+                                           gemm_routes.route_table().items() if v),
         }
         print(json.dumps(out), flush=True)
     if dist.is_initialized():

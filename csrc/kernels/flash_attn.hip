@@ -100,7 +100,71 @@ struct Frag {
     r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
     return r;
   }
+  // All D/32 transposed fragments of (t, ss) -- tr(tile, t, ss, 0..D/32-1) --
+  // issued from inline asm; the caller waits with tr_wait() before use.
+  // Why: for the builtin form the compiler's wait-count pass cannot tell the
+  // read from the LDS-DMA prefetch of the NEXT tile still in flight, and puts
+  // an s_waitcnt vmcnt(0) before the first transposed read of every loop
+  // iteration (gfx950 assembly of fa_fwd / fa_bwd_dq / fa_bwd_dkdv), so the
+  // prefetch overlapped only the first half of a tile.  The tile read here
+  // was completed by the previous iteration's vmcnt(0) + barrier.
+  __device__ __forceinline__ void tr_issue(const char* tile, int t, int ss,
+                                           v4s (&lo)[D / 32], v4s (&hi)[D / 32]) const {
+    const uint32_t base = (uint32_t)(size_t)((const __attribute__((address_space(3))) char*)tile);
+    const uint32_t a0 = base + tb0 + 64 * D * t + 32 * D * ss;
+    const uint32_t a1 = base + tb1 + 64 * D * t + 32 * D * ss;
+    if constexpr (D == 64) {
+      asm volatile(
+          "ds_read_b64_tr_b16 %0, %4\n\t"
+          "ds_read_b64_tr_b16 %1, %5\n\t"
+          "ds_read_b64_tr_b16 %2, %4 offset:512\n\t"
+          "ds_read_b64_tr_b16 %3, %5 offset:512"
+          : "=&v"(lo[0]), "=&v"(hi[0]), "=&v"(lo[1]), "=&v"(hi[1])
+          : "v"(a0), "v"(a1));
+    } else if constexpr (D == 96) {
+      asm volatile(
+          "ds_read_b64_tr_b16 %0, %6\n\t"
+          "ds_read_b64_tr_b16 %1, %7\n\t"
+          "ds_read_b64_tr_b16 %2, %6 offset:512\n\t"
+          "ds_read_b64_tr_b16 %3, %7 offset:512\n\t"
+          "ds_read_b64_tr_b16 %4, %6 offset:1024\n\t"
+          "ds_read_b64_tr_b16 %5, %7 offset:1024"
+          : "=&v"(lo[0]), "=&v"(hi[0]), "=&v"(lo[1]), "=&v"(hi[1]), "=&v"(lo[2]), "=&v"(hi[2])
+          : "v"(a0), "v"(a1));
+    } else {
+      asm volatile(
+          "ds_read_b64_tr_b16 %0, %8\n\t"
+          "ds_read_b64_tr_b16 %1, %9\n\t"
+          "ds_read_b64_tr_b16 %2, %8 offset:512\n\t"
+          "ds_read_b64_tr_b16 %3, %9 offset:512\n\t"
+          "ds_read_b64_tr_b16 %4, %8 offset:1024\n\t"
+          "ds_read_b64_tr_b16 %5, %9 offset:1024\n\t"
+          "ds_read_b64_tr_b16 %6, %8 offset:1536\n\t"
+          "ds_read_b64_tr_b16 %7, %9 offset:1536"
+          : "=&v"(lo[0]), "=&v"(hi[0]), "=&v"(lo[1]), "=&v"(hi[1]), "=&v"(lo[2]), "=&v"(hi[2]),
+            "=&v"(lo[3]), "=&v"(hi[3])
+          : "v"(a0), "v"(a1));
+    }
+  }
 };
+
+// Wait for tr_issue() results (and any other LDS / scalar-memory op in flight):
+// the registers are operands, so no use can be scheduled above the wait.
+template <int ND>
+__device__ __forceinline__ void tr_wait(v4s (&lo)[ND], v4s (&hi)[ND]) {
+  if constexpr (ND == 2)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo[0]), "+v"(hi[0]), "+v"(lo[1]), "+v"(hi[1]));
+  else if constexpr (ND == 3)
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(lo[0]), "+v"(hi[0]), "+v"(lo[1]), "+v"(hi[1]), "+v"(lo[2]), "+v"(hi[2]));
+  else
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(lo[0]), "+v"(hi[0]), "+v"(lo[1]), "+v"(hi[1]), "+v"(lo[2]), "+v"(hi[2]),
+                   "+v"(lo[3]), "+v"(hi[3]));
+}
+__device__ __forceinline__ short8 tr_join(const v4s& lo, const v4s& hi) {
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
 
 // bf16 or fp16 inputs (T), fp32 accumulate; the 16-bit operands travel as raw lanes
 template <typename T>
@@ -397,12 +461,15 @@ __device__ __forceinline__ void fwd_tile(const AttnParams& P, const Frag<D>& F, 
       if (t == 1 && !half2) continue;  // P = 0 there
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
+        v4s vlo[D / 32], vhi[D / 32];
+        F.tr_issue(vt, t, ss, vlo, vhi);
         short8 pf;
 #pragma unroll
         for (int j = 0; j < 8; ++j) pf[j] = cvt16<T>(sacc[t][8 * ss + j]);
+        tr_wait(vlo, vhi);
 #pragma unroll
         for (int dt = 0; dt < D / 32; ++dt)
-          oacc[dt] = mfma<T>(F.tr(vt, t, ss, dt), pf, oacc[dt]);
+          oacc[dt] = mfma<T>(tr_join(vlo[dt], vhi[dt]), pf, oacc[dt]);
       }
     }
   }
@@ -657,12 +724,15 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
         }
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
+          v4s klo[D / 32], khi[D / 32];
+          F.tr_issue(kt, t, ss, klo, khi);
           short8 df;
 #pragma unroll
           for (int j = 0; j < 8; ++j) df[j] = cvt16<T>(sacc[8 * ss + j]);
+          tr_wait(klo, khi);
 #pragma unroll
           for (int dt = 0; dt < D / 32; ++dt)
-            dqacc[dt] = mfma<T>(F.tr(kt, t, ss, dt), df, dqacc[dt]);
+            dqacc[dt] = mfma<T>(tr_join(klo[dt], khi[dt]), df, dqacc[dt]);
         }
       }
     }
@@ -882,11 +952,22 @@ __device__ __forceinline__ void dkdv_body(const AttnParams& P, char* smem) {
               df[j] = cvt16<T>(p * (dpacc[i] - dl_s[ql_]));  // dS
             }
           }
+          // (issued after P / dS are packed: the register budget of D = 128
+          // has no room for the fragments while the tile's fp32 values live)
+          v4s glo[D / 32], ghi[D / 32];
+          F.tr_issue(gt, t, ss, glo, ghi);
+          tr_wait(glo, ghi);
 #pragma unroll
-          for (int dt = 0; dt < D / 32; ++dt) {
-            dvacc[dt] = mfma<T>(F.tr(gt, t, ss, dt), pf, dvacc[dt]);
-            dkacc[dt] = mfma<T>(F.tr(qt, t, ss, dt), df, dkacc[dt]);
-          }
+          for (int dt = 0; dt < D / 32; ++dt)
+            dvacc[dt] = mfma<T>(tr_join(glo[dt], ghi[dt]), pf, dvacc[dt]);
+          // the Q fragments only after the dO ones are consumed: D = 128 has
+          // no registers for both sets at once
+          v4s qlo[D / 32], qhi[D / 32];
+          F.tr_issue(qt, t, ss, qlo, qhi);
+          tr_wait(qlo, qhi);
+#pragma unroll
+          for (int dt = 0; dt < D / 32; ++dt)
+            dkacc[dt] = mfma<T>(tr_join(qlo[dt], qhi[dt]), df, dkacc[dt]);
         }
       }
     }

@@ -114,8 +114,12 @@ def out_tiles(kind, a, b, t=128):
 # stream) and the kernel takes the shape only when it wins by ROUTE_MARGIN,
 # so near-ties stay on one side from run to run.  The vendor path of a kind
 # is registered by its caller (VENDOR).
+# Forward GEMMs are not raced: their timing in isolation misleads, since in
+# the step they share the chip with the forward-overlapped AdamW, which a
+# gemm5 forward (whole CUs per workgroup) starves (6.7B: one run whose race
+# sent forward shapes to the kernel took 313 ms vs 293; profiles/r4_route/).
 ROUTE_TUNE = os.environ.get("FLEETX_GEMM_ROUTE", "tune") == "tune"
-TUNE_KINDS = ("fwd", "dgrad")
+TUNE_KINDS = ("dgrad",)
 ROUTE_MARGIN = 0.03
 VENDOR = {}
 _ROUTE = {}
