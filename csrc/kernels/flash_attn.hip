@@ -280,6 +280,7 @@ __device__ __forceinline__ void glds_wait() { asm volatile("s_waitcnt vmcnt(0)" 
 // row max is subtracted, and flushing results below 2^-126 to zero is exact
 // enough for softmax -- libm exp2f adds a denormal-range fix-up per element.
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 struct AttnParams {
   const uint16_t *q, *k, *v, *o, *dout;
@@ -368,9 +369,13 @@ __device__ __forceinline__ void fwd_tile(const AttnParams& P, const Frag<D>& F, 
   // waves without a valid query (the tail block of S = 257) only help load
   if (wq0 < P.Sq && !(CAUSAL && kb > wq0 + 31)) {
     floatx16 sacc[2];
-    // the tile's second 32-key half is skipped (scores -inf, no MFMAs) when
-    // every key in it is past kv_len (the tail tile of S = 257) or above the
-    // causal diagonal of all this wave's queries (wave-uniform)
+    // the tile's second 32-key half holds no unmasked key when every key in
+    // it is past kv_len (the tail tile of S = 257) or above the causal
+    // diagonal of all this wave's queries (wave-uniform); its P.V MFMAs are
+    // skipped below.  Its scores are still computed (and masked to -inf by
+    // the diagonal / tail pass): skipping those MFMAs too made the compiler
+    // copy the first half's 16 accumulators on every tile to merge the two
+    // paths, which cost more than the few MFMAs it saved on diagonal tiles.
     const bool half2 = (kb + 32 < kv_len && !(CAUSAL && kb + 32 > wq0 + 31));
     // all K fragments of the tile up front: the 16 LDS reads overlap each
     // other instead of one exposed LDS latency per MFMA
@@ -378,15 +383,9 @@ __device__ __forceinline__ void fwd_tile(const AttnParams& P, const Frag<D>& F, 
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s)
-        if (t == 0 || half2) kfr[t][s] = F.row(kt, t, s);
+      for (int s = 0; s < D / 16; ++s) kfr[t][s] = F.row(kt, t, s);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      if (t == 1 && !half2) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sacc[t][i] = -INFINITY;
-        continue;
-      }
 #pragma unroll
       for (int i = 0; i < 16; ++i) sacc[t][i] = 0.f;
 #pragma unroll
@@ -433,19 +432,22 @@ __device__ __forceinline__ void fwd_tile(const AttnParams& P, const Frag<D>& F, 
           for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
       }
       const float m_use = (m_run == -INFINITY) ? 0.f : m_run;
+      // score pairs in packed fp32 (v_pk_fma_f32 / v_pk_add_f32: two lanes'
+      // worth per VALU issue; the softmax VALU, not the MFMAs, bounds the
+      // causal and D = 64 tiles)
+      const f2 nm = {-m_use, -m_use}, sc2 = {sl2, sl2};
+      // four independent partial sums (a single dependent chain of packed
+      // adds stalls on the packed-VALU read-after-write hazard)
+      f2 lacc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int i = 0; i < 16; i += 2) {
-          float p0, p1;
-          if constexpr (KB) {
-            p0 = fexp2(sacc[t][i] - m_use);
-            p1 = fexp2(sacc[t][i + 1] - m_use);
-          } else {
-            p0 = fexp2(__builtin_fmaf(sacc[t][i], sl2, -m_use));
-            p1 = fexp2(__builtin_fmaf(sacc[t][i + 1], sl2, -m_use));
-          }
-          lsum += p0 + p1;
+          const f2 sv = {sacc[t][i], sacc[t][i + 1]};
+          const f2 a = KB ? sv + nm : __builtin_elementwise_fma(sv, sc2, nm);
+          const f2 pv = {fexp2(a.x), fexp2(a.y)};
+          lacc[(i >> 1) & 3] += pv;
+          float p0 = pv.x, p1 = pv.y;
           if (DROP) {  // the keep scale 1/(1-p) is applied once, to O
             const int key = kb + 32 * t + crow(i, h);  // even
             const uint32_t hh = lowbias32((((uint32_t)qi) << 16 | ((uint32_t)key >> 1)) ^ cb);
@@ -455,6 +457,8 @@ __device__ __forceinline__ void fwd_tile(const AttnParams& P, const Frag<D>& F, 
           sacc[t][i] = p0;
           sacc[t][i + 1] = p1;
         }
+      const f2 lt = (lacc[0] + lacc[1]) + (lacc[2] + lacc[3]);
+      lsum += lt.x + lt.y;
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -1007,7 +1011,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
 template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_q64v_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  dkdv_body<T, D, CAUSAL, DROP, KB, 64, true>(P, smem);
+  // launched for D <= 96 only (D = 128 has no registers for V; it would spill)
+  if constexpr (D <= 96) dkdv_body<T, D, CAUSAL, DROP, KB, 64, true>(P, smem);
 }
 
 AttnParams make_params(const void* q, const void* k, const void* v, const long* qs,
