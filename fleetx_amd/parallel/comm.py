@@ -130,6 +130,28 @@ class IpcAllReduce:
         self._last = None  # (stream, event) of the previous call
         # every rank must have mapped every peer before anyone writes into it
         dist.barrier(group=pg)
+        self._self_test(pg)
+
+    def _self_test(self, pg, bound_s=5.0):
+        """One all-reduce of known values under a short wait bound, agreed by
+        every rank: a receive area the peers cannot reach (no peer mapping
+        over xGMI, a refused IPC import that still returned a pointer, ...)
+        then disables the path at setup instead of stalling the first training
+        step for the full timeout and skipping it."""
+        n = max(1, min(256, self.max_bytes // 4))
+        probe = torch.full((n,), float(self.rank + 1), dtype=torch.float32, device=self.device)
+        saved = self.timeout_ticks
+        self.timeout_ticks = int(bound_s * _TICKS_PER_S)
+        try:
+            self.all_reduce(probe)
+        finally:
+            self.timeout_ticks = saved
+        expect = float(self.world * (self.world + 1) // 2)
+        ok = int(self.err.item()) == 0 and bool((probe == expect).all())
+        self.err.zero_()
+        if not _agree(ok, pg, self.device):
+            self.close()
+            raise RuntimeError("one-shot all-reduce self-test failed on group %s" % self.name)
 
     def supports(self, t, op=dist.ReduceOp.SUM):
         return (t.is_cuda and t.dtype in _DT and op in _OPS and t.is_contiguous()
