@@ -27,8 +27,11 @@ _HCG = None
 # RCCL channel is one workgroup resident on a CU for the whole collective, so
 # the budget is set per group by what the group overlaps with, not by one
 # process-wide NCCL_MIN_NCHANNELS:
-#  * mp (TP all-reduce / SP gather-scatter): on the critical path, nothing to
-#    share the CUs with -> many channels;
+#  * mp (TP all-reduce / SP gather-scatter): on the critical path -> many
+#    channels when the group spans several links; a TP-2 pair is ONE xGMI
+#    link, which a few channels fill, so its default only caps the count
+#    (every extra channel is a CU taken from the GEMM chunk the all-reduce
+#    overlaps; RCCL's topology search picks the rest) -- see model_ctas();
 #  * dp / sharding / data_world (gradient buckets, ZeRO gathers): overlapped
 #    with backward GEMMs that want all 256 CUs -> capped;
 #  * pp (activation p2p) and the tied-embedding pair: medium;
@@ -39,6 +42,15 @@ CTA_KEYS = {"dp": "data", "mp": "model", "pp": "pipe", "sharding": "sharding",
 DEFAULT_CTAS = {"model": (32, 64), "data": (8, 16), "sharding": (8, 16),
                 "data_world": (8, 16), "pipe": (4, 16), "check": (1, 4),
                 "embedding": (8, 32)}
+
+
+def model_ctas(t):
+    """Default TP-group budget for a group of ``t`` GPUs: ``t - 1`` links."""
+    if t <= 2:
+        return (None, 16)
+    if t <= 4:
+        return (8, 32)
+    return DEFAULT_CTAS["model"]
 
 
 def parse_ctas(cfg):
@@ -162,6 +174,7 @@ class HybridCommunicateGroup:
         self.stage_id = self.pp_rank
         self._nccl = self.initialized and dist.get_backend() == "nccl"
         self.ctas = parse_ctas(ctas) if ctas is not False else {}
+        self._model_ctas_set = bool(ctas) and any(CTA_KEYS.get(k, k) == "model" for k in ctas)
 
         self._groups = {}
         for axis in HybridTopology.AXES:
@@ -182,9 +195,16 @@ class HybridCommunicateGroup:
         self._groups["pipe_bwd"] = self._build(self.topo.axis_groups("pipe"), "pipe_bwd") \
             if pp > 1 and pp_split_directions else self._groups["pipe"]
 
+    def ctas_for(self, name):
+        """Effective ``(min, max)`` CTA budget of group ``name`` (or None)."""
+        c = self.ctas.get(name)
+        if name == "model" and c is not None and not self._model_ctas_set:
+            c = model_ctas(self.mp_degree)
+        return c
+
     def pg_options(self, name):
         """RCCL options of group ``name`` (None on gloo or without a budget)."""
-        return nccl_options(self.ctas.get(name)) if self._nccl else None
+        return nccl_options(self.ctas_for(name)) if self._nccl else None
 
     def _build(self, rank_lists, name):
         mine = None
@@ -327,66 +347,6 @@ def set_hcg(hcg):
 def reset_hcg():
     global _HCG
     _HCG = None
-
-# Per-communicator RCCL CTA budget (``Distributed.comm.ctas.<key>``): every
-# RCCL channel is one workgroup resident on a CU for the whole collective, so
-# the budget is set per group by what the group overlaps with, not by one
-# process-wide NCCL_MIN_NCHANNELS:
-#  * mp (TP all-reduce / SP gather-scatter): on the critical path, nothing to
-#    share the CUs with -> many channels;
-#  * dp / sharding / data_world (gradient buckets, ZeRO gathers): overlapped
-#    with backward GEMMs that want all 256 CUs -> capped;
-#  * pp (activation p2p) and the tied-embedding pair: medium;
-#  * check (norm / found-inf scalars): latency-bound -> few.
-# ``(min_ctas, max_ctas)``; ``None`` leaves the bound to RCCL.
-CTA_KEYS = {"dp": "data", "mp": "model", "pp": "pipe", "sharding": "sharding",
-            "data_world": "data_world", "check": "check", "embedding": "embedding"}
-DEFAULT_CTAS = {"model": (32, 64), "data": (8, 16), "sharding": (8, 16),
-                "data_world": (8, 16), "pipe": (4, 16), "check": (1, 4),
-                "embedding": (8, 32)}
-
-
-def parse_ctas(cfg):
-    """``Distributed.comm.ctas`` -> ``{group name: (min, max)}`` over the
-    defaults.  Values: ``"min,max"``, ``[min, max]`` or an int (max only);
-    ``None`` / ``False`` for a key drops the bound; ``ctas: False`` drops all."""
-    if cfg is False:
-        return {}
-    out = dict(DEFAULT_CTAS)
-    for k, v in dict(cfg or {}).items():
-        name = CTA_KEYS.get(k, k)
-        if name not in DEFAULT_CTAS:
-            raise ValueError("Distributed.comm.ctas: unknown group %r (keys: %s)"
-                             % (k, ", ".join(sorted(CTA_KEYS))))
-        if v in (None, False):
-            out.pop(name, None)
-            continue
-        if isinstance(v, str):
-            v = [int(x) for x in v.split(",")]
-            v = v[0] if len(v) == 1 else v
-        if isinstance(v, int):
-            v = (None, v)
-        lo, hi = v
-        if lo is not None and hi is not None and lo > hi:
-            raise ValueError("Distributed.comm.ctas.%s: min %d > max %d" % (k, lo, hi))
-        out[name] = (lo, hi)
-    out["pipe_bwd"] = out.get("pipe")
-    if out["pipe_bwd"] is None:
-        out.pop("pipe_bwd")
-    return out
-
-
-def nccl_options(ctas):
-    """``ProcessGroupNCCL.Options`` carrying ``(min_ctas, max_ctas)``."""
-    if ctas is None:
-        return None
-    opts = dist.ProcessGroupNCCL.Options()
-    lo, hi = ctas
-    if lo is not None:
-        opts.config.min_ctas = int(lo)
-    if hi is not None:
-        opts.config.max_ctas = int(hi)
-    return opts
     from . import comm
     comm.reset()
 

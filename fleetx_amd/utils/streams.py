@@ -112,7 +112,8 @@ def inventory(hcg=None, optimizer=None, buffer=None, wgrad_stream=False):
             if g is None or g.group is None or id(g.group) in seen:
                 continue
             seen.add(id(g.group))
-            c = getattr(hcg, "ctas", {}).get(name) if getattr(hcg, "_nccl", False) else None
+            c = hcg.ctas_for(name) if getattr(hcg, "_nccl", False) and hasattr(hcg, "ctas_for") \
+                else None
             budget = "" if c is None else "(ctas %s-%s)" % (c[0] or "auto", c[1] or "auto")
             out.append(("rccl:%s%s%s" % (name, list(g.ranks), budget), True))
     return out

@@ -4,7 +4,7 @@ set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r4b5
 mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gemm_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gemm_gpu.py tests/test_comm_gpu.py tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit 1
 G=4:1,0:0,8:4,4:4,8:2,4:2,8:1
 for h in 1024 1408 2048; do

@@ -1,9 +1,11 @@
 """Host-side launch plans of the HIP kernels, checked on the CPU (the plan
 code runs without a GPU; the CU count falls back to MI355X's 256):
 
-* gemm5 split-K for fp32 weight gradients (csrc/kernels/gemm5.hip
-  ``g5_split_plan``): only a last wave at most a quarter full is split, the
-  slab workspace is R tiles x S slices x TILE^2 fp32;
+* gemm5 geometry / split-K for fp32 weight gradients (csrc/kernels/gemm5.hip
+  ``g5_f32_nf`` + ``g5_split_plan``): 256-tiles cut into <= 4 slices for
+  48-128 of them, 128-tile grids under 384 tiles cut to about one workgroup
+  per CU, otherwise only a last wave at most a quarter full is split; the
+  slab workspace is tiles x S slices x TILE^2 fp32;
 * the one-pass LayerNorm backward (csrc/kernels/norm_eltwise.hip
   ``fx_ln_bwd_cols_blocks``): covered widths and partial-row counts."""
 import os
@@ -27,15 +29,19 @@ def test_splitk_plan():
     k = _k()
     # ViT-g FC1 weight gradient: 48 x 11 128-tiles = 528 on 512 slots -> 16 tiles x 32 slices
     assert k.gemm_ws_bytes(EPI_F32, 6144, 1408, 16448) == 16 * 32 * 128 * 128 * 4
-    # ViT-g out-proj: 121 tiles -> 4 slices of K 16448
-    assert k.gemm_ws_bytes(EPI_F32, 1408, 1408, 16448) == 121 * 4 * 128 * 128 * 4
-    # 345M out-proj: 64 tiles, K 8192 -> 8 slices
-    assert k.gemm_ws_bytes(EPI_F32, 1024, 1024, 8192) == 64 * 8 * 128 * 128 * 4
-    # whole waves (6.7B: 256-tiles fill 256 slots) and half-full last waves never split
+    # ViT-g out-proj: 121 128-tiles -> round(256 / 121) = 2 slices
+    assert k.gemm_ws_bytes(EPI_F32, 1408, 1408, 16448) == 121 * 2 * 128 * 128 * 4
+    # 345M out-proj: 64 128-tiles -> 4 slices
+    assert k.gemm_ws_bytes(EPI_F32, 1024, 1024, 8192) == 64 * 4 * 128 * 128 * 4
+    # 345M QKV (48 256-tiles) -> 256-tiles in 4 slices; ViT-g QKV (102) -> 2
+    assert k.gemm_ws_bytes(EPI_F32, 3072, 1024, 8192) == 48 * 4 * 256 * 256 * 4
+    assert k.gemm_ws_bytes(EPI_F32, 4224, 1408, 8192) == 102 * 2 * 256 * 256 * 4
+    # whole waves (6.7B: 256-tiles fill 256 slots) never split
     assert k.gemm_ws_bytes(EPI_F32, 4096, 4096, 8192) == 0
     assert k.gemm_ws_bytes(EPI_F32, 12288, 4096, 8192) == 0
-    assert k.gemm_ws_bytes(EPI_F32, 2048, 2048, 8192) == 0
-    # short K: at least 4 K-tiles per slice
+    # 129-191 256-tiles: 128-tiles, unsplit at >= 384 of them (ViT-g FC1 at 8192 tokens)
+    assert k.gemm_ws_bytes(EPI_F32, 5632, 1408, 8192) == 0
+    # short K: at least 8 K-tiles per slice
     assert k.gemm_ws_bytes(EPI_F32, 1024, 1024, 256) == 0
     # only the fp32 weight-gradient epilogue splits
     assert k.gemm_ws_bytes(0, 6144, 1408, 16448) == 0
