@@ -243,7 +243,7 @@ def test_tile_order_autotune_is_bitwise_neutral(gemm):
 
 
 def test_route_tuner_picks_a_path_and_both_agree():
-    """Per-shape routing of plain forward / data-gradient GEMMs (ops/gemm.py
+    """Per-shape routing of plain data-gradient GEMMs (ops/gemm.py
     _tuned_route): the first call of a shape races the MFMA kernel against the
     registered vendor path, caches the winner, and either path matches fp32."""
     from fleetx_amd.ops import gemm as G
@@ -261,13 +261,14 @@ def test_route_tuner_picks_a_path_and_both_agree():
         y = L.fwd_gemm(x, w)
         dx = L.dgrad_gemm(dy, w)
         table = G.route_table()
-        assert ("fwd", M, N, K) in table and ("dgrad", M, K, N) in table
+        # data gradients race; forward GEMMs do not (see ops/gemm.py)
+        assert ("dgrad", M, K, N) in table and ("fwd", M, N, K) not in table
         assert _rel(y, x.float() @ w.float().t()) < 1e-2
         assert _rel(dx, dy.float() @ w.float()) < 1e-2
         # small outputs never race (under MIN_TILES): vendor path, cached False
-        xs = torch.randn(256, K, device="cuda", dtype=torch.bfloat16)
-        L.fwd_gemm(xs, w[:512])
-        assert G.route_table()[("fwd", 256, 512, K)] is False
+        dys = torch.randn(256, 512, device="cuda", dtype=torch.bfloat16)
+        L.dgrad_gemm(dys, w[:512])
+        assert G.route_table()[("dgrad", 256, K, 512)] is False
     finally:
         G.set_mode(old[0])
         G.ROUTE_TUNE = old[1]
