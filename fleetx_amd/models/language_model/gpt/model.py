@@ -168,6 +168,10 @@ class GPTMLP(nn.Module):
         self.fc2 = L.RowParallelLinear(cfg.ffn_hidden_size, cfg.hidden_size, bias=True,
                                        skip_bias_add=True, sequence_parallel=cfg.sequence_parallel,
                                        std=std, name="layers.%d.mlp.fc2" % idx, dtype=cfg.dtype)
+        # FC1 -> bias+GeLU -> FC2 is row-wise in between: under overlapped
+        # SP the intermediate stays in chunk-major row order (one GEMM per
+        # chunk instead of one per rank per chunk; parallel/sp_overlap.py)
+        self.fc1.sp_chunk_major = self.fc2.sp_chunk_major = bool(cfg.sequence_parallel)
 
     def forward(self, x):
         if topo.mp_world_size() == 1 and type(self.fc1) is L.ColumnParallelLinear \

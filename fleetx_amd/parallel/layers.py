@@ -114,7 +114,8 @@ class ColumnParallelLinear(nn.Module):
         b = None if self.skip_bias_add else self.bias
         if self.sequence_parallel:
             if TP_OVERLAP["enabled"] and x.dim() == 3:
-                y = column_sp_linear(x, self.weight, b, topo.mp_group())
+                y = column_sp_linear(x, self.weight, b, topo.mp_group(),
+                                     chunk_major=getattr(self, "sp_chunk_major", False))
             else:
                 x = M.all_gather_seq(x)
                 y = linear(x, self.weight, b)
@@ -165,9 +166,14 @@ class RowParallelLinear(nn.Module):
         if not self.input_is_parallel:
             x = M.scatter_to_mp(x)
         if self.sequence_parallel:
-            if TP_OVERLAP["enabled"] and x.dim() == 3 and x.shape[0] % topo.mp_world_size() == 0:
-                y = row_sp_linear(x, self.weight, topo.mp_group())
+            # chunk-major input exactly when the paired column-SP linear took
+            # its overlapped path (same TP_OVERLAP / rank-3 conditions)
+            overlap = TP_OVERLAP["enabled"] and x.dim() == 3
+            cm = overlap and getattr(self, "sp_chunk_major", False)
+            if overlap and x.shape[0] % topo.mp_world_size() == 0:
+                y = row_sp_linear(x, self.weight, topo.mp_group(), chunk_major=cm)
             else:
+                assert not cm, "a chunk-major input needs the overlapped row-SP path"
                 y = M.reduce_scatter_seq(linear(x, self.weight))
         elif topo.mp_world_size() > 1 and TP_OVERLAP["enabled"]:
             y = row_tp_linear(x, self.weight, topo.mp_group(), TP_OVERLAP["row_chunks"])

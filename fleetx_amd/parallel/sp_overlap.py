@@ -17,13 +17,25 @@ stream waits per chunk):
   reduce-scatter posted at once, the weight gradient accumulates chunk by
   chunk in fp32 (``main_grad``) under the reduce-scatters;
 * row (fwd): per chunk, ``t`` GEMMs into a staging block, reduce-scatter
-  posted at once -> the next chunk's GEMMs hide it;
+  posted at once -> the next chunk's GEMMs hide it.  The last chunk's
+  scatter is exposed: the output feeds the residual add and LayerNorm of
+  every row, and the next linear's gather needs those; hiding it would mean
+  running the next layer's norm and gather chunk by chunk as well;
 * row (bwd): chunked all-gather of the output gradient, dgrad / wgrad per
   chunk as it lands.
 
 On xGMI the ring collectives are per-link bandwidth bound, so ``c = 2`` (two
 half-size collectives) already hides most of the transfer behind GEMMs of a
 GPT-3 layer; more chunks only add launch latency.
+
+Chunk-major layout (``chunk_major=True``, the MLP's FC1 -> GeLU -> FC2):
+the full-sequence activation between a column-SP and a row-SP linear is
+only ever touched row-wise (bias + GeLU), so its rows may be kept in
+(chunk, rank, row) order instead of sequence order.  Sub-chunk ``k`` of
+every rank is then ONE contiguous ``[t * s/(t c) * b, .]`` block, and each
+chunk is a single GEMM instead of ``t`` (FC1 forward / data gradient, FC2
+forward / data gradient, and both weight gradients).  Attention needs the
+sequence order, so QKV and the output projection keep it.
 """
 import torch
 import torch.distributed as dist
@@ -85,21 +97,24 @@ def _wgrad_chunks(weight, pairs, want_bias):
 
 class _ColumnSP(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, g, c):
+    def forward(ctx, x, weight, bias, g, c, cm):
         t = g.nranks
         S, B, h = x.shape
         n = weight.shape[0]
         sc = S // c
         gathered = _post_ag(x, g, c)
         y = torch.empty(t * S, B, n, dtype=x.dtype, device=x.device)
-        yv = y.view(t, c, sc * B, n)
+        yv = y.view(c, t * sc * B, n) if cm else y.view(t, c, sc * B, n)
         bufs = []
         for k, (w, buf, _) in enumerate(gathered):
             w.wait()
-            for r in range(t):
-                _mm_into(buf[r].view(sc * B, h), weight, yv[r, k], bias)
+            if cm:  # chunk k of every rank: one GEMM into one contiguous block
+                _mm_into(buf.view(t * sc * B, h), weight, yv[k], bias)
+            else:
+                for r in range(t):
+                    _mm_into(buf[r].view(sc * B, h), weight, yv[r, k], bias)
             bufs.append(buf)
-        ctx.g, ctx.c, ctx.has_bias = g, c, bias is not None
+        ctx.g, ctx.c, ctx.cm, ctx.has_bias = g, c, cm, bias is not None
         ctx.shape = (S, B, h, n)
         ctx.save_for_backward(weight, *bufs)
         return y
@@ -107,75 +122,89 @@ class _ColumnSP(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         weight, *bufs = ctx.saved_tensors
-        g, c = ctx.g, ctx.c
+        g, c, cm = ctx.g, ctx.c, ctx.cm
         t = g.nranks
         S, B, h, n = ctx.shape
         sc = S // c
-        dyv = dy.contiguous().view(t, c, sc * B, n)
+        dyv = dy.contiguous().view(c, t * sc * B, n) if cm else dy.contiguous().view(t, c, sc * B, n)
         dx = torch.empty(S, B, h, dtype=dy.dtype, device=dy.device)
         works = []
         for k in range(c):
             stage = torch.empty(t, sc * B, h, dtype=dy.dtype, device=dy.device)
-            for r in range(t):
-                _dgrad_into(dyv[r, k], weight, stage[r])
+            if cm:
+                _dgrad_into(dyv[k], weight, stage.view(t * sc * B, h))
+            else:
+                for r in range(t):
+                    _dgrad_into(dyv[r, k], weight, stage[r])
             works.append((dist.reduce_scatter_tensor(dx[k * sc:(k + 1) * sc].view(sc * B, h),
                                                      stage.view(t * sc * B, h), group=g.group,
                                                      async_op=True), stage))
-        pairs = [(dyv[r, k], bufs[k][r].view(sc * B, h)) for k in range(c) for r in range(t)]
+        if cm:
+            pairs = [(dyv[k], bufs[k].view(t * sc * B, h)) for k in range(c)]
+        else:
+            pairs = [(dyv[r, k], bufs[k][r].view(sc * B, h)) for k in range(c) for r in range(t)]
         dw, db = _wgrad_chunks(weight, pairs, ctx.has_bias)
         for w, _ in works:
             w.wait()
         if db is not None:
             db = db.to(weight.dtype)
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
 class _RowSP(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, g, c):
+    def forward(ctx, x, weight, g, c, cm):
         t = g.nranks
         S_full, B, hin = x.shape
         S = S_full // t
         n = weight.shape[0]
         sc = S // c
-        xv = x.contiguous().view(t, c, sc * B, hin)
+        xv = x.contiguous().view(c, t * sc * B, hin) if cm else x.contiguous().view(t, c, sc * B, hin)
         y = torch.empty(S, B, n, dtype=x.dtype, device=x.device)
         works = []
         for k in range(c):
             stage = torch.empty(t, sc * B, n, dtype=x.dtype, device=x.device)
-            for r in range(t):
-                _mm_into(xv[r, k], weight, stage[r])
+            if cm:
+                _mm_into(xv[k], weight, stage.view(t * sc * B, n))
+            else:
+                for r in range(t):
+                    _mm_into(xv[r, k], weight, stage[r])
             works.append((dist.reduce_scatter_tensor(y[k * sc:(k + 1) * sc].view(sc * B, n),
                                                      stage.view(t * sc * B, n), group=g.group,
                                                      async_op=True), stage))
         for w, _ in works:
             w.wait()
-        ctx.g, ctx.c = g, c
+        ctx.g, ctx.c, ctx.cm = g, c, cm
         ctx.save_for_backward(x, weight)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
-        g, c = ctx.g, ctx.c
+        g, c, cm = ctx.g, ctx.c, ctx.cm
         t = g.nranks
         S_full, B, hin = x.shape
         S = S_full // t
         n = weight.shape[0]
         sc = S // c
-        xv = x.contiguous().view(t, c, sc * B, hin)
+        xv = x.contiguous().view(c, t * sc * B, hin) if cm else x.contiguous().view(t, c, sc * B, hin)
         gathered = _post_ag(dy.contiguous(), g, c)
         dx = torch.empty(S_full, B, hin, dtype=dy.dtype, device=dy.device)
-        dxv = dx.view(t, c, sc * B, hin)
+        dxv = dx.view(c, t * sc * B, hin) if cm else dx.view(t, c, sc * B, hin)
         pairs = []
         for k, (w, buf, _) in enumerate(gathered):
             w.wait()
-            for r in range(t):
-                dyb = buf[r].view(sc * B, n)
-                _dgrad_into(dyb, weight, dxv[r, k])
-                pairs.append((dyb, xv[r, k]))
+            if cm:
+                dyb = buf.view(t * sc * B, n)
+                _dgrad_into(dyb, weight, dxv[k])
+                pairs.append((dyb, xv[k]))
+            else:
+                for r in range(t):
+                    dyb = buf[r].view(sc * B, n)
+                    _dgrad_into(dyb, weight, dxv[r, k])
+                    pairs.append((dyb, xv[r, k]))
         dw, _ = _wgrad_chunks(weight, pairs, False)
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 def _chunks_for(S):
@@ -185,14 +214,18 @@ def _chunks_for(S):
     return c
 
 
-def column_sp_linear(x, weight, bias, group):
-    """``all_gather_seq(x) @ W^T (+ b)`` with the gather overlapped."""
-    return _ColumnSP.apply(x, weight, bias, group, _chunks_for(x.shape[0]))
+def column_sp_linear(x, weight, bias, group, chunk_major=False):
+    """``all_gather_seq(x) @ W^T (+ b)`` with the gather overlapped; rows in
+    (chunk, rank, row) order with ``chunk_major`` (feed a chunk-major
+    :func:`row_sp_linear` only)."""
+    return _ColumnSP.apply(x, weight, bias, group, _chunks_for(x.shape[0]), bool(chunk_major))
 
 
-def row_sp_linear(x, weight, group):
-    """``reduce_scatter_seq(x @ W^T)`` with the scatter overlapped."""
-    return _RowSP.apply(x, weight, group, _chunks_for(x.shape[0] // group.nranks))
+def row_sp_linear(x, weight, group, chunk_major=False):
+    """``reduce_scatter_seq(x @ W^T)`` with the scatter overlapped; ``x`` in
+    the chunk-major row order of a chunk-major :func:`column_sp_linear`."""
+    return _RowSP.apply(x, weight, group, _chunks_for(x.shape[0] // group.nranks),
+                        bool(chunk_major))
 
 
 __all__ = ["column_sp_linear", "row_sp_linear", "SP_CHUNKS", "grad_part_done"]
