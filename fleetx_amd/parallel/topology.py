@@ -29,7 +29,7 @@ _HCG = None
 # process-wide NCCL_MIN_NCHANNELS:
 #  * mp (TP all-reduce / SP gather-scatter): on the critical path -> many
 #    channels when the group spans several links; a TP-2 pair is ONE xGMI
-#    link, which a few channels fill, so its default only caps the count
+#    link, which a few channels fill, so its budget is small
 #    (every extra channel is a CU taken from the GEMM chunk the all-reduce
 #    overlaps; RCCL's topology search picks the rest) -- see model_ctas();
 #  * dp / sharding / data_world (gradient buckets, ZeRO gathers): overlapped
@@ -45,11 +45,13 @@ DEFAULT_CTAS = {"model": (32, 64), "data": (8, 16), "sharding": (8, 16),
 
 
 def model_ctas(t):
-    """Default TP-group budget for a group of ``t`` GPUs: ``t - 1`` links."""
+    """Default TP-group budget for a group of ``t`` GPUs: ``t - 1`` links,
+    about 8 channels per link (unmeasured across GPUs: a floor so one link is
+    kept busy, a cap so the overlapped GEMM keeps its CUs)."""
     if t <= 2:
-        return (None, 16)
+        return (8, 16)
     if t <= 4:
-        return (8, 32)
+        return (16, 32)
     return DEFAULT_CTAS["model"]
 
 

@@ -61,13 +61,13 @@ def test_options_reach_new_group():
     for ranks, lo, hi in seen:
         by.setdefault((lo, hi), []).append(ranks)
     assert (4, 12) in by and (0, 4) in by[(4, 12)]          # dp groups: ranks differ by 4
-    # mp groups (adjacent ranks): a TP-2 pair is one xGMI link -> only a cap
-    assert (None, 16) in by and (0, 1) in by[(None, 16)]
+    # mp groups (adjacent ranks): a TP-2 pair is one xGMI link -> small budget
+    assert (8, 16) in by and (0, 1) in by[(8, 16)]
     assert (4, 16) in by and (0, 2) in by[(4, 16)]          # pp groups
-    assert any("rccl:model[0, 1](ctas auto-16)" == n for n in res[0]["inv"])
+    assert any("rccl:model[0, 1](ctas 8-16)" == n for n in res[0]["inv"])
 
 
 def test_model_budget_scales_with_group_size():
-    assert topo.model_ctas(2) == (None, 16)
-    assert topo.model_ctas(4) == (8, 32)
+    assert topo.model_ctas(2) == (8, 16)
+    assert topo.model_ctas(4) == (16, 32)
     assert topo.model_ctas(8) == topo.DEFAULT_CTAS["model"] == (32, 64)
