@@ -115,9 +115,10 @@ def out_tiles(kind, a, b, t=128):
 # so near-ties stay on one side from run to run.  The vendor path of a kind
 # is registered by its caller (VENDOR).
 # Forward GEMMs are not raced: their timing in isolation misleads, since in
-# the step they share the chip with the forward-overlapped AdamW, which a
-# gemm5 forward (whole CUs per workgroup) starves (6.7B: one run whose race
-# sent forward shapes to the kernel took 313 ms vs 293; profiles/r4_route/).
+# the step they share the chip with the forward-overlapped AdamW.  With the
+# QKV forward on gemm5 (10 % faster alone) the 6.7B step takes 316-317 ms
+# vs 293-295 (three interleaved runs each; ViT-g 461 vs 465 img/s;
+# profiles/r4_route/fwd_race_ab.txt).
 ROUTE_TUNE = os.environ.get("FLEETX_GEMM_ROUTE", "tune") == "tune"
 TUNE_KINDS = ("dgrad",)
 ROUTE_MARGIN = 0.03
