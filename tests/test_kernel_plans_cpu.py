@@ -27,8 +27,8 @@ def _k():
 
 def test_splitk_plan():
     k = _k()
-    # ViT-g FC1 weight gradient: 48 x 11 128-tiles = 528 on 512 slots -> 16 tiles x 32 slices
-    assert k.gemm_ws_bytes(EPI_F32, 6144, 1408, 16448) == 16 * 32 * 128 * 128 * 4
+    # 528 128-tiles on 512 slots (short K: 256 K-tiles is the ViT rule below) -> 16 tiles x 32 slices
+    assert k.gemm_ws_bytes(EPI_F32, 6144, 1408, 8192) == 16 * 32 * 128 * 128 * 4
     # ViT-g out-proj: 121 128-tiles -> round(256 / 121) = 2 slices
     assert k.gemm_ws_bytes(EPI_F32, 1408, 1408, 16448) == 121 * 2 * 128 * 128 * 4
     # 345M out-proj: 64 128-tiles -> 4 slices
@@ -39,8 +39,11 @@ def test_splitk_plan():
     # whole waves (6.7B: 256-tiles fill 256 slots) never split
     assert k.gemm_ws_bytes(EPI_F32, 4096, 4096, 8192) == 0
     assert k.gemm_ws_bytes(EPI_F32, 12288, 4096, 8192) == 0
-    # 129-191 256-tiles: 128-tiles, unsplit at >= 384 of them (ViT-g FC1 at 8192 tokens)
+    # 129-191 256-tiles: 128-tiles, unsplit at >= 384 of them (ViT-g FC1 at 8192 tokens) ...
     assert k.gemm_ws_bytes(EPI_F32, 5632, 1408, 8192) == 0
+    # ... but 256-tiles in 3 slices over >= 192 K-tiles (ViT-g FC1 / FC2 at 16448 tokens)
+    assert k.gemm_ws_bytes(EPI_F32, 6144, 1408, 16448) == 144 * 3 * 256 * 256 * 4
+    assert k.gemm_ws_bytes(EPI_F32, 1408, 6144, 16448) == 144 * 3 * 256 * 256 * 4
     # short K: at least 8 K-tiles per slice
     assert k.gemm_ws_bytes(EPI_F32, 1024, 1024, 256) == 0
     # only the fp32 weight-gradient epilogue splits

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--geom", default="", help="comma list of nf:split lab geometries for the "
                                                "hip_wgrad cases, e.g. 4:1,4:2,8:4 (0:0 = plan)")
+    ap.add_argument("--ffn", type=int, default=0, help="MLP width (default 4 x hidden)")
     ap.add_argument("--vocab", type=int, default=0, help="also time the LM head (h -> vocab)")
     ap.add_argument("--only", default="", help="comma list of case names")
     ap.add_argument("--gm", default="", help="comma list of tile-order M-group heights to A/B "
@@ -43,7 +44,8 @@ def main():
     from fleetx_amd.ops import gemm as G
     M, h = a.tokens, a.hidden
     dev, bf = "cuda", torch.bfloat16
-    shapes = {"qkv": (h, 3 * h), "out": (h, h), "fc1": (h, 4 * h), "fc2": (4 * h, h)}
+    ffn = a.ffn or 4 * h
+    shapes = {"qkv": (h, 3 * h), "out": (h, h), "fc1": (h, ffn), "fc2": (ffn, h)}
     if a.vocab:
         shapes["head"] = (h, a.vocab)
     for name, (K, N) in shapes.items():
