@@ -583,14 +583,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
 // backward dQ: WG = 4 waves x 32 queries; loop over 64-key tiles.
 //   S^T = K.Q^T, dP^T = V.dO^T (queries on lanes), dQ^T += K^T.dS^T
 // ============================================================================
-template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
-__global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
+template <typename T, int D, bool CAUSAL, bool DROP, bool KB, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int KV = 64, TB = KV * D * 2;
+  constexpr int KV = 64, TB = KV * D * 2, QB = 32 * NW;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
   Frag<D> F;
   F.init(lane);
-  const int nq = (P.Sq + 127) / 128;
+  const int nq = (P.Sq + QB - 1) / QB;
   const int nblk = nq * P.B * P.H;
   const int lid = xcd_remap(blockIdx.x, nblk);
   int bh, qblock;
@@ -610,7 +610,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
   int kv_len = P.Sk;
   if (P.kv_lens) kv_len = min(kv_len, P.kv_lens[b]);
 
-  const int wq0 = qblock * 128 + w * 32;
+  const int wq0 = qblock * QB + w * 32;
   const int qi = wq0 + (lane & 31);
   const bool qvalid = qi < P.Sq;
   short8 qf[D / 16], gf[D / 16];
@@ -630,7 +630,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
   const uint32_t cb = DROP ? attn_cb(P, bh) : 0u;
 
   int kv_end = kv_len;
-  if (CAUSAL) kv_end = min(kv_end, (qblock + 1) * 128);
+  if (CAUSAL) kv_end = min(kv_end, (qblock + 1) * QB);
   const int ntiles = (kv_end + KV - 1) / KV;
 
   floatx16 dqacc[D / 32];
@@ -639,7 +639,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(AttnParams P) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) dqacc[dt][i] = 0.f;
 
-  GldsStream<D, KV> kld, vld;
+  GldsStream<D, KV, NW> kld, vld;
   kld.init(kp, P.sk_s, kv_end, w, lane, P.dval);
   vld.init(vp, P.sv_s, kv_end, w, lane, P.dval);
   if (ntiles > 0) {
@@ -785,8 +785,9 @@ __device__ __forceinline__ uint32_t dpp_swap1(uint32_t v) {
 // QT: query rows per tile (32, or 64 = half the barriers / DMA issue points
 // per unit of work); VREG: this wave's V rows in 32 VGPRs instead of a
 // 128-row LDS image (keeps two workgroups per CU at QT = 64).
-template <typename T, int D, bool CAUSAL, bool DROP, bool KB, int QT, bool VREG>
+template <typename T, int D, bool CAUSAL, bool DROP, bool KB, int QT, bool VREG, int NW = 4>
 __device__ __forceinline__ void dkdv_body(const AttnParams& P, char* smem) {
+  constexpr int KR = 32 * NW;  // keys per workgroup
   constexpr int TB = QT * D * 2;
   // one buffer: [Q tile][dO tile][lse2 QT floats][delta QT floats]; then V rows
   constexpr int BUF = 2 * TB + 2 * QT * 4;
@@ -794,7 +795,7 @@ __device__ __forceinline__ void dkdv_body(const AttnParams& P, char* smem) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
   Frag<D> F;
   F.init(lane);
-  const int nk = (P.Sk + 127) / 128;
+  const int nk = (P.Sk + KR - 1) / KR;
   const int nblk = nk * P.B * P.H;
   const int lid = xcd_remap(blockIdx.x, nblk);
   int bh, kblock;  // causal: low key blocks are the heavy ones
@@ -812,7 +813,7 @@ __device__ __forceinline__ void dkdv_body(const AttnParams& P, char* smem) {
   int kv_len = P.Sk;
   if (P.kv_lens) kv_len = min(kv_len, P.kv_lens[b]);
 
-  const int wk0 = kblock * 128 + w * 32;
+  const int wk0 = kblock * KR + w * 32;
   const int ki = wk0 + (lane & 31);
   const bool kvalid = ki < kv_len;
   // per-key additive term of the exp2 argument; -inf masks keys past kv_len
@@ -837,7 +838,7 @@ __device__ __forceinline__ void dkdv_body(const AttnParams& P, char* smem) {
         vf[s] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
     }
   } else {
-    Glds<D, 128>::load(vp, P.sv_s, kblock * 128, P.Sk, vs, w, lane, P.dval);
+    Glds<D, KR, NW>::load(vp, P.sv_s, kblock * KR, P.Sk, vs, w, lane, P.dval);
   }
   floatx16 dkacc[D / 32], dvacc[D / 32];
 #pragma unroll
@@ -847,7 +848,7 @@ __device__ __forceinline__ void dkdv_body(const AttnParams& P, char* smem) {
   const float sl2 = P.scale * LOG2E;
   const uint32_t cb = DROP ? attn_cb(P, bh) : 0u;
 
-  const int q_begin = CAUSAL ? (kblock * 128 / QT) * QT : 0;
+  const int q_begin = CAUSAL ? (kblock * KR / QT) * QT : 0;
   const int ntiles = P.Sq > q_begin ? (P.Sq - q_begin + QT - 1) / QT : 0;
   // row constants of tile qb: loaded BEFORE the tile's DMA is issued (vmcnt
   // retires in order), written to LDS after the compute of the current tile
@@ -866,7 +867,7 @@ __device__ __forceinline__ void dkdv_body(const AttnParams& P, char* smem) {
       c[QT + tid] = nd;
     }
   };
-  GldsStream<D, QT> qld, gld;
+  GldsStream<D, QT, NW> qld, gld;
   qld.init(qp, P.sq_s, P.Sq, w, lane, P.dval);
   gld.init(dop, P.so_s, P.Sq, w, lane, P.dval);
   if (ntiles > 0) {
@@ -1008,11 +1009,11 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   dkdv_body<T, D, CAUSAL, DROP, KB, FA_DKDV_QT, false>(P, smem);
 }
-template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
-__global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_q64v_kernel(AttnParams P) {
+template <typename T, int D, bool CAUSAL, bool DROP, bool KB, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dkdv_q64v_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // launched for D <= 96 only (D = 128 has no registers for V; it would spill)
-  if constexpr (D <= 96) dkdv_body<T, D, CAUSAL, DROP, KB, 64, true>(P, smem);
+  if constexpr (D <= 96) dkdv_body<T, D, CAUSAL, DROP, KB, 64, true, NW>(P, smem);
 }
 
 AttnParams make_params(const void* q, const void* k, const void* v, const long* qs,
@@ -1067,6 +1068,16 @@ static void fa_fwd_dispatch(bool causal, bool drop, bool kbias, int grid, size_t
 
 static int tile_dim(int d) { return d <= 64 ? 64 : (d <= 96 ? 96 : 128); }
 
+// Waves per workgroup (32 rows each) along a sequence of n rows for the
+// 96-wide tile: 3 when that leaves fewer idle waves than 4.  ViT-g's 257
+// tokens are 9 row tiles: 3 x 3 waves with none idle, against 3 x 4 with 3
+// idle waves holding the last workgroup's slots for a single row.
+static int waves_for(int n) {
+  const int tiles = (n + 31) / 32;
+  const int idle3 = (n + 95) / 96 * 3 - tiles, idle4 = (n + 127) / 128 * 4 - tiles;
+  return idle3 < idle4 ? 3 : 4;
+}
+
 static int fwd_waves() {
   static int nw = [] {
     const char* e = getenv("FLEETX_FA_FWD_WAVES");
@@ -1088,6 +1099,20 @@ static int fwd_waves() {
       if (drop) fa_launch(KERNEL<T, DD, false, true, false>, grid, smem, st, P); \
       else fa_launch(KERNEL<T, DD, false, false, false>, grid, smem, st, P);     \
     }                                                                           \
+  } while (0)
+// one tile width with NW waves per workgroup (block size 64 NW)
+#define FA_DISPATCH_NW(KERNEL, DD, NW, causal, drop, kbias, grid, smem, st, P)                  \
+  do {                                                                                        \
+    if (causal) {                                                                             \
+      if (drop) fa_launch(KERNEL<T, DD, true, true, false, NW>, grid, smem, st, P, 64 * NW);  \
+      else fa_launch(KERNEL<T, DD, true, false, false, NW>, grid, smem, st, P, 64 * NW);      \
+    } else if (kbias) {                                                                       \
+      if (drop) fa_launch(KERNEL<T, DD, false, true, true, NW>, grid, smem, st, P, 64 * NW);  \
+      else fa_launch(KERNEL<T, DD, false, false, true, NW>, grid, smem, st, P, 64 * NW);      \
+    } else {                                                                                  \
+      if (drop) fa_launch(KERNEL<T, DD, false, true, false, NW>, grid, smem, st, P, 64 * NW); \
+      else fa_launch(KERNEL<T, DD, false, false, false, NW>, grid, smem, st, P, 64 * NW);     \
+    }                                                                                         \
   } while (0)
 // key bias is only instantiated for non-causal attention (BERT-style padding
 // masks); causal + bias is rejected by the launchers.
@@ -1120,7 +1145,7 @@ static int flash_fwd_t(const void* q, const void* k, const void* v, void* out, f
   P.kbias = kbias;
   P.kb_b = kb_stride;
   P.so_b = os[0]; P.so_s = os[1]; P.so_h = os[2];
-  const int nw = D == 96 ? 4 : fwd_waves();
+  const int nw = D == 96 ? waves_for(Sq) : fwd_waves();
   const int nq = (Sq + 32 * nw - 1) / (32 * nw);
   const int grid = nq * B * H;
   const size_t smem = 4 * 64 * D * 2;
@@ -1130,6 +1155,7 @@ static int flash_fwd_t(const void* q, const void* k, const void* v, void* out, f
     else fa_fwd_dispatch<T, 64, 8>(causal, drop, kb, grid, smem, st, P);
   } else {
     if (D == 128) fa_fwd_dispatch<T, 128, 4>(causal, drop, kb, grid, smem, st, P);
+    else if (D == 96 && nw == 3) fa_fwd_dispatch<T, 96, 3>(causal, drop, kb, grid, smem, st, P);
     else if (D == 96) fa_fwd_dispatch<T, 96, 4>(causal, drop, kb, grid, smem, st, P);
     else fa_fwd_dispatch<T, 64, 4>(causal, drop, kb, grid, smem, st, P);
   }
@@ -1163,17 +1189,27 @@ static int flash_bwd_t(const void* q, const void* k, const void* v, const void* 
   P.so_b = os[0]; P.so_s = os[1]; P.so_h = os[2];
   P.sdk_b = dks[0]; P.sdk_s = dks[1]; P.sdk_h = dks[2];
   P.sdq_b = dqs[0]; P.sdq_s = dqs[1]; P.sdq_h = dqs[2];
+  const bool drop = p > 0.f, kb = kbias != nullptr;
   {
-    const int nq = (Sq + 127) / 128;
     const size_t smem = 4 * 64 * D * 2;
-    FA_DISPATCH(fa_bwd_dq_kernel, D, causal, p > 0.f, kbias != nullptr, nq * B * H, smem, st, P);
+    if (D == 96 && waves_for(Sq) == 3) {
+      const int nq = (Sq + 95) / 96;
+      FA_DISPATCH_NW(fa_bwd_dq_kernel, 96, 3, causal, drop, kb, nq * B * H, smem, st, P);
+    } else {
+      const int nq = (Sq + 127) / 128;
+      FA_DISPATCH(fa_bwd_dq_kernel, D, causal, drop, kb, nq * B * H, smem, st, P);
+    }
   }
   {
-    const int nk = (Sk + 127) / 128;
     // double-buffered Q/dO tiles + row constants, then the WG's V rows
     // D <= 96: 64-query tiles with V in registers (bwd 0.150 -> 0.144 ms at
     // B8 S1024 H16 D64, profiles/r3_dkdv/); D = 128 has no 32 VGPRs to spare.
-    if (D <= 96) {
+    const int nk = (Sk + 127) / 128;
+    if (D == 96 && waves_for(Sk) == 3) {
+      const size_t smem = 2 * (2 * 64 * D * 2 + 2 * 64 * 4);
+      FA_DISPATCH_NW(fa_bwd_dkdv_q64v_kernel, 96, 3, causal, drop, kb, (Sk + 95) / 96 * B * H,
+                     smem, st, P);
+    } else if (D <= 96) {
       const size_t smem = 2 * (2 * 64 * D * 2 + 2 * 64 * 4);
       FA_DISPATCH(fa_bwd_dkdv_q64v_kernel, D, causal, p > 0.f, kbias != nullptr, nk * B * H,
                   smem, st, P);

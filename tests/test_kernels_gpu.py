@@ -493,6 +493,29 @@ def test_flash_attention_padded_head_dim(D):
         assert _rel(a.grad, r.grad) < 3e-2
 
 
+@pytest.mark.parametrize("S", [257, 190, 96])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_flash_attention_three_wave_tiles(S, causal, p):
+    """96-wide tiles over row counts where 3-wave workgroups leave fewer idle
+    waves (flash_attn.hip waves_for: ViT-g's 257 tokens): forward, dQ and
+    dK/dV with 96-row workgroups, causal and dropout included, vs fp32."""
+    from fleetx_amd import ops
+    B, H, D = 2, 3, 88
+    key = 1234
+    qkv = (0.5 * torch.randn(B, S, 3, H, D, device=DEV)).bfloat16().requires_grad_()
+    out = ops.flash_attention_qkvpacked(qkv, causal=causal, dropout_p=p, key=key, pack_dim=2)
+    ref_in = qkv.detach().float().requires_grad_()
+    ref = ops.attention_reference(ref_in[:, :, 0], ref_in[:, :, 1], ref_in[:, :, 2],
+                                  causal=causal, dropout_p=p, key=key)
+    assert _rel(out, ref) < 2e-2, _rel(out, ref)
+    g = torch.randn_like(ref)
+    out.backward(g.bfloat16())
+    ref.backward(g)
+    for i in range(3):
+        assert _rel(qkv.grad[:, :, i], ref_in.grad[:, :, i]) < 3e-2, (i, _rel(qkv.grad[:, :, i], ref_in.grad[:, :, i]))
+
+
 def test_vit_train_step_on_gpu():
     from fleetx_amd.models.vision_model.vit import ViT
     from fleetx_amd.models.vision_model.loss import ViTCELoss
