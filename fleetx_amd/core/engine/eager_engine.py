@@ -232,13 +232,16 @@ class EagerEngine(BasicEngine):
                     decr_every=int(amp.get("decr_every_n_nan_or_inf", 2)),
                     device=self.device)
                 self.optimizer.loss_scale = self.scaler.scale
-            # weight-gradient GEMMs beside the data-gradient chain (parallel/linear.py);
-            # opt-in: two library GEMMs in flight on two streams can deadlock when
-            # both are stream-K kernels waiting for workgroups the other holds
-            # (seen on ViT-g shapes), for a +1.5 % gain on 345M / 1.3B
-            ws = comm.get("wgrad_stream", False)
+            # weight-gradient GEMMs beside the data-gradient chain (parallel/linear.py;
+            # only gemm5 launches go there: two library stream-K GEMMs in flight
+            # on two streams can deadlock).  "auto" (default): models whose GEMMs
+            # under-fill the chip (hidden <= 2048) outside whole-step graph mode
+            # -- 1.3B 71.7 -> 70.3 ms; 345M in its graph 30.1 -> 30.6 ms, so off
+            # there; profiles/r4_wgs/
+            ws = comm.get("wgrad_stream", "auto")
             if ws == "auto":
-                ws = configs.Model.get("hidden_size", 0) <= 2048
+                ws = configs.Model.get("hidden_size", 0) <= 2048 and \
+                    not bool(e.get("cuda_graph", False))
             from ...parallel import linear as _lin
             _lin.WGRAD_STREAM["enabled"] = bool(ws) and self.device.type == "cuda" \
                 and type(self.buffer) is FlatParamGradBuffer
