@@ -114,11 +114,14 @@ def out_tiles(kind, a, b, t=128):
 # stream) and the kernel takes the shape only when it wins by ROUTE_MARGIN,
 # so near-ties stay on one side from run to run.  The vendor path of a kind
 # is registered by its caller (VENDOR).
-# Forward GEMMs are not raced: their timing in isolation misleads, since in
-# the step they share the chip with the forward-overlapped AdamW.  With the
+# Forward GEMMs are not raced: their isolated timing misleads in the step.
+# Beside the forward-overlapped AdamW a gemm5 wave takes its SIMD's whole
+# register file, so the update cannot share those CUs:  With the
 # QKV forward on gemm5 (10 % faster alone) the 6.7B step takes 316-317 ms
 # vs 293-295 (three interleaved runs each; ViT-g 461 vs 465 img/s;
-# profiles/r4_route/fwd_race_ab.txt).
+# profiles/r4_route/fwd_race_ab.txt).  Even without the overlapped update
+# (345M in its graph) the race's picks (out-proj, FC2 forward) made the step
+# 0.1-0.3 ms slower (profiles/r4_route/fwd_race_345m.txt).
 ROUTE_TUNE = os.environ.get("FLEETX_GEMM_ROUTE", "tune") == "tune"
 TUNE_KINDS = ("dgrad",)
 ROUTE_MARGIN = 0.03

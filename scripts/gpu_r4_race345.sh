@@ -1,0 +1,13 @@
+#!/bin/bash
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r4race345
+mkdir -p $O
+run() {
+  env $2 timeout -k 10 300 python -u bench.py $3 > $O/$1.log 2>&1 || { tail -5 $O/$1.log; exit 1; }
+  echo "$1 $(tail -1 $O/$1.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["value"], d["mfu"], d.get("gemm_raced_to_kernel"))')" | tee -a $O/summary.txt
+}
+for r in 1 2; do
+  run s345_auto_$r "X=1" "--model gpt-345M --steps 20 --warmup 5"
+  run s345_dgrad_$r "FLEETX_BENCH_OVERRIDES=Distributed.comm.gemm_race_forward=False" "--model gpt-345M --steps 20 --warmup 5"
+done
