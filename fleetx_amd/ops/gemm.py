@@ -104,7 +104,7 @@ def out_tiles(kind, a, b, t=128):
     return _tiles(a.shape[-1], b.shape[-1], t)
 
 
-# Per-shape routing of the plain forward / data-gradient GEMMs
+# Per-shape routing of the plain data-gradient GEMMs
 # (FLEETX_GEMM_ROUTE=tune, the default; "off" keeps the kind table alone).
 # Which of the MFMA kernel and hipBLASLt is faster depends on the shape
 # (GPT-3 6.7B with the tuned tile order: QKV forward 1466 vs 1331 TF/s, FC1
@@ -116,7 +116,7 @@ def out_tiles(kind, a, b, t=128):
 # is registered by its caller (VENDOR).
 # Forward GEMMs are not raced: their isolated timing misleads in the step.
 # Beside the forward-overlapped AdamW a gemm5 wave takes its SIMD's whole
-# register file, so the update cannot share those CUs:  With the
+# register file, so the update cannot share those CUs: with the
 # QKV forward on gemm5 (10 % faster alone) the 6.7B step takes 316-317 ms
 # vs 293-295 (three interleaved runs each; ViT-g 461 vs 465 img/s;
 # profiles/r4_route/fwd_race_ab.txt).  Even without the overlapped update
