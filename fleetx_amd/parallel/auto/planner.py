@@ -28,7 +28,7 @@ from dataclasses import asdict, dataclass
 
 HBM_BYTES = 288e9
 USABLE = 0.85            # leave room for the caching allocator / workspace
-SUSTAINED_FLOPS = 1.12e15  # measured: 6.7B 1-GPU step at ~45% of 2.5 PF/s (profiles/r2_step2)
+SUSTAINED_FLOPS = 1.16e15  # measured: 6.7B 1-GPU step, 293.7 ms (profiles/r4_full3)
 # effective per-direction xGMI bandwidth per link: ~153 GB/s nominal x ~65 % RCCL
 # efficiency (an assumption -- the development box has one GPU; recalibrate from
 # SCALE_*.json once multi-GPU runs exist)
