@@ -252,11 +252,14 @@ class EagerEngine(BasicEngine):
             # step N's AdamW runs on a side stream under step N+1's forward (also
             # with the fp16 loss scaler: its found-inf / scale live on the device
             # and the next step() joins the side stream before rewriting them)
-            if comm.get("overlap_optimizer", True) and not self._pipeline and not self._cuda_graph \
+            # (in whole-step graph mode the update is deferred into the next
+            # step's captured body: FlatOptimizer.launch_pending)
+            if comm.get("overlap_optimizer", True) and not self._pipeline \
                     and hasattr(self.optimizer, "enable_forward_overlap"):
                 self.optimizer.overlap_grid = int(comm.get("overlap_optimizer_grid", 128))
                 self.optimizer.overlap_cus = int(comm.get("overlap_optimizer_cus", 0) or 0)
-                self.optimizer.enable_forward_overlap(model)
+                if self.optimizer.enable_forward_overlap(model) and self._cuda_graph:
+                    self.optimizer.defer_update = True
             # single data rank: gradient sum-of-squares per bucket under backward
             # (opt-in: measured neutral on 6.7B, the GEMMs leave no CU slots free)
             if comm.get("early_grad_norm", False) and not self._pipeline and not self._cuda_graph \
@@ -325,17 +328,29 @@ class EagerEngine(BasicEngine):
         self._graph_salt = torch.full((1,), getattr(self, "_graph_salt_resume", 0),
                                       dtype=torch.int64, device=self.device)
         self._graph_lr = torch.zeros(1, dtype=torch.float32, device=self.device)
+        # deferred update (optimizer.defer_update): it runs one step later and
+        # reads the learning rate of its own step, copied here by each body
+        self._graph_lr_pending = torch.zeros(1, dtype=torch.float32, device=self.device)
         k.set_dropout_salt(self._graph_salt.data_ptr())
-        k.set_adamw_lr_ptr(self._graph_lr.data_ptr())
+        k.set_adamw_lr_ptr((self._graph_lr_pending if self._defer_update() else
+                            self._graph_lr).data_ptr())
         # the kernels read these process-global device pointers: clear them when
         # this engine goes away (unless a newer engine has taken them over), so
         # a later engine / optimizer never reads freed memory
         _GRAPH_PTR_OWNER[0] = id(self)
         weakref.finalize(self, _release_graph_ptrs, id(self))
 
+    def _defer_update(self):
+        return bool(getattr(self.optimizer, "defer_update", False))
+
     def _graph_body(self, batch):
         """The device work of one step: fresh dropout salt, forward, backward,
-        gradient finish, clip + AdamW, gradient reset."""
+        gradient finish, clip + AdamW, gradient reset.  With the deferred
+        overlapped update the previous step's AdamW starts first, on the side
+        stream, under this step's forward."""
+        defer = self._defer_update()
+        if defer:
+            self.optimizer.launch_pending()
         self._graph_salt.add_(1)
         model = self._module.model
         model.train()
@@ -352,6 +367,8 @@ class EagerEngine(BasicEngine):
         self.buffer.finish()
         self.optimizer.step()
         self.optimizer.clear_grad()
+        if defer:
+            self._graph_lr_pending.copy_(self._graph_lr)
         return loss
 
     def _graph_batch_matches(self, batch):
@@ -395,6 +412,8 @@ class EagerEngine(BasicEngine):
                     dst.copy_(src, non_blocking=True)
             self._graph.replay()
             self.optimizer.step_count += 1  # the captured step() ran its host part once
+            if self._defer_update():
+                self.optimizer._pending = self.optimizer.get_lr()  # this replay's update
             # the captured loss is one static tensor that every replay rewrites:
             # hand out a copy (fit() accumulates it across steps)
             loss = self._graph_loss.clone()
@@ -474,6 +493,8 @@ class EagerEngine(BasicEngine):
                 break
         if self._profiler:
             self._profiler.stop()
+        if self.optimizer is not None:
+            self.optimizer.sync_state()  # the last (overlapped / deferred) update lands
         if torch.cuda.is_available():
             torch.cuda.synchronize()
             _comm.check_all()
@@ -571,6 +592,7 @@ class EagerEngine(BasicEngine):
     # ------------------------------------------------------------------ eval
     @torch.no_grad()
     def _evaluate_impl(self, epoch, loader, iters):
+        self._flush_deferred_update()
         model = self._module.model
         model.eval()
         outs = []
@@ -602,7 +624,12 @@ class EagerEngine(BasicEngine):
         model.train()
         return outs
 
+    def _flush_deferred_update(self):
+        if getattr(self, "optimizer", None) is not None and self._defer_update():
+            self.optimizer.sync_state()  # the last step's update has not started yet
+
     def evaluate(self, epoch=1, valid_data_loader=None):
+        self._flush_deferred_update()
         model = self._module.model
         model.eval()
         outs = []
@@ -622,6 +649,7 @@ class EagerEngine(BasicEngine):
 
     @torch.no_grad()
     def predict(self, epoch=1, test_data_loader=None):
+        self._flush_deferred_update()
         model = self._module.model
         model.eval()
         outs = []

@@ -168,8 +168,26 @@ class FlatOptimizer:
         self._prepare_scale()
         self.step_count += 1
         self.dev_step.add_(1 - self.found_inf)
-        self._update(self.get_lr())
+        if self.defer_update and self._overlap_groups is not None:
+            self._pending = self.get_lr()  # launched by the next step (launch_pending)
+        else:
+            self._update(self.get_lr())
         self.buffer.allgather_params()
+
+    # Whole-step graph mode (Engine.cuda_graph): the forward-overlapped update
+    # of step N is launched at the START of step N+1's captured body, so one
+    # replay holds both it and the forward it overlaps (a graph cannot wait
+    # on work launched outside it).  Clip scale, found-inf and the Adam step
+    # come from step N's device state; the learning rate from the device
+    # buffer the engine copies at the end of each body.
+    defer_update = False
+    _pending = None
+
+    def launch_pending(self):
+        """Deferred mode: start the previous step's update on the side stream."""
+        if self._pending is not None:
+            lr, self._pending = self._pending, None
+            self._update_overlapped(lr)
 
     # ------------------------------------------------------------------ overlap
     _overlap_groups = None
@@ -261,7 +279,13 @@ class FlatOptimizer:
 
     def sync_state(self):
         """Wait for the last update: host-offloaded D2H copies, or the
-        forward-overlapped update stream."""
+        forward-overlapped update stream (a deferred one is applied now)."""
+        if self._pending is not None:
+            self.launch_pending()
+            # a captured step launches this update again at its start: with
+            # the skip flag set it leaves the applied update alone (the step's
+            # own found-inf is recomputed after its backward)
+            self.found_inf.fill_(1)
         self._join_overlap()
         cs = getattr(self, "_copy_stream", None)
         if cs is not None:

@@ -13,7 +13,7 @@ CFG = os.path.join(os.path.dirname(__file__), "..", "fleetx_amd", "configs", "nl
                    "pretrain_gpt_345M_single_card.yaml")
 
 
-def _engine(graph, drop, lr=None, steps=8):
+def _engine(graph, drop, lr=None, steps=8, extra=()):
     from fleetx_amd.utils import config as C
     from fleetx_amd.utils import env
     from fleetx_amd.models import build_module
@@ -29,6 +29,7 @@ def _engine(graph, drop, lr=None, steps=8):
           "Global.device=gpu", "Global.local_batch_size=4", "Global.micro_batch_size=4",
           "Engine.max_steps=%d" % steps, "Engine.mix_precision.dtype=bfloat16",
           "Engine.cuda_graph=%s" % graph, "Data.Train.dataset.name=SyntheticGPTDataset"]
+    ov += list(extra)
     cfg = C.get_config(CFG, overrides=ov, nranks=1)
     if lr is not None:
         cfg.Optimizer.lr = {"name": "ConstantLR", "learning_rate": lr}
@@ -117,3 +118,31 @@ def test_graph_short_batch_runs_eagerly():
     from fleetx_amd.ops import _lib
     _lib.kernels().set_dropout_salt(0)
     _lib.kernels().set_adamw_lr_ptr(0)
+
+
+def test_graph_with_deferred_overlapped_update_matches_serial(monkeypatch):
+    """Graph mode runs step N's AdamW at the start of step N+1's captured body,
+    beside its forward (optimizer.defer_update): parameters after the last
+    step (flushed by sync_state) are bitwise those of the graph with the
+    serial update, and a flush in between is not applied twice."""
+    monkeypatch.setenv("FLEETX_DETERMINISTIC", "1")
+    bs = _batches(7)
+    ser = _engine(True, 0.0, extra=["Distributed.comm.overlap_optimizer=False"])
+    assert not ser.optimizer.defer_update
+    _run(ser, bs)
+    ser.optimizer.sync_state()
+    torch.cuda.synchronize()
+    eng = _engine(True, 0.0)
+    assert eng.optimizer.defer_update and eng._cuda_graph
+    losses = _run(eng, bs[:5])
+    assert eng._graph is not None
+    eng.optimizer.sync_state()          # applies step 5's update (flush)
+    mid = {n: p.detach().clone() for n, p in eng._module.model.named_parameters()}
+    _run(eng, bs[5:])                   # the flushed update is not applied twice
+    eng.optimizer.sync_state()
+    torch.cuda.synchronize()
+    for (n, a), (_, b) in zip(ser._module.model.named_parameters(),
+                              eng._module.model.named_parameters()):
+        assert torch.equal(a, b), n
+    assert any(not torch.equal(mid[n], p) for n, p in eng._module.model.named_parameters())
+    assert all(l == l for l in losses)
