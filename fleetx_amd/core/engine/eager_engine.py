@@ -493,7 +493,7 @@ class EagerEngine(BasicEngine):
                 break
         if self._profiler:
             self._profiler.stop()
-        if self.optimizer is not None:
+        if getattr(self.optimizer, "sync_state", None) is not None:
             self.optimizer.sync_state()  # the last (overlapped / deferred) update lands
         if torch.cuda.is_available():
             torch.cuda.synchronize()
