@@ -280,13 +280,16 @@ class FlatOptimizer:
     def sync_state(self):
         """Wait for the last update: host-offloaded D2H copies, or the
         forward-overlapped update stream (a deferred one is applied now)."""
-        if self._pending is not None:
+        flushed = self._pending is not None
+        if flushed:
             self.launch_pending()
+        self._join_overlap()
+        if flushed:
             # a captured step launches this update again at its start: with
             # the skip flag set it leaves the applied update alone (the step's
-            # own found-inf is recomputed after its backward)
+            # own found-inf is recomputed after its backward).  Set only after
+            # the join: the update itself reads the flag
             self.found_inf.fill_(1)
-        self._join_overlap()
         cs = getattr(self, "_copy_stream", None)
         if cs is not None:
             cs.synchronize()
