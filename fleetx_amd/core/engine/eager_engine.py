@@ -260,10 +260,15 @@ class EagerEngine(BasicEngine):
                 self.optimizer.overlap_cus = int(comm.get("overlap_optimizer_cus", 0) or 0)
                 if self.optimizer.enable_forward_overlap(model) and self._cuda_graph:
                     self.optimizer.defer_update = True
-                    # uncapped in the graph (345M: 29.07-29.28 ms vs 29.20-29.58
-                    # at the 128-workgroup cap, serial 29.27-29.32;
-                    # profiles/r4_defer/)
-                    self.optimizer.overlap_grid = int(comm.get("overlap_optimizer_grid", 0))
+                    # uncapped in the graph for hidden <= 1024 (345M: 29.07-29.28
+                    # ms vs 29.20-29.58 at the 128-workgroup cap, serial
+                    # 29.27-29.32; profiles/r4_defer/); larger models keep the
+                    # cap (6.7B 293.7-294.4 ms at 128 vs 297.0-298.7 uncapped,
+                    # 64: 306.8, 192: 297.3-298.7; 1.3B 70.4-70.5 vs 71.4;
+                    # profiles/r4_g67/)
+                    small = configs.Model.get("hidden_size", 0) <= 1024
+                    self.optimizer.overlap_grid = int(comm.get("overlap_optimizer_grid",
+                                                               0 if small else 128))
             # single data rank: gradient sum-of-squares per bucket under backward
             # (opt-in: measured neutral on 6.7B, the GEMMs leave no CU slots free)
             if comm.get("early_grad_norm", False) and not self._pipeline and not self._cuda_graph \
