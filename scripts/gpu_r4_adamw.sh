@@ -1,5 +1,6 @@
 #!/bin/bash
 # AdamW kernel variants (non-temporal mode x block shape) at full grid and the 128 cap.
+# (ran with profiles/r4_adamw/variants.patch applied; the --variants sweep was not kept)
 set -o pipefail
 O=gpurun_out/r4adamw
 mkdir -p $O

@@ -1,5 +1,6 @@
 #!/bin/bash
 # Stored-dS attention backward: numerics, then old (recompute) vs new attention bench.
+# (ran with profiles/r4_ds/stored_ds.patch applied; FLEETX_FA_BWD_DS was not kept)
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r4ds

@@ -1,5 +1,6 @@
 #!/bin/bash
 # Per-kernel split of the stored-dS vs recompute attention backward (D128 causal and D64).
+# (ran with profiles/r4_ds/stored_ds.patch applied; FLEETX_FA_BWD_DS was not kept)
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r4dsprof
