@@ -21,7 +21,10 @@ runs the planner's choice (micro-batch 8, no recompute for 6.7B).
 bandwidth, 1F1B bubble, ZeRO traffic and the 288 GB budget), and
 ``--layout dp,mp,pp,micro[,sharding[,stage]]`` pins one.  The JSON line's
 ``config.parallelism`` names the layout.  Weak scaling: 8 sequences x 1024
-tokens of work per GPU per step.
+tokens of work per GPU per step.  On one GPU the step is captured as one HIP
+graph during the warmup (``--hip-graph``; needs ``--warmup >= 3``) and
+replayed for the K timed steps, each replay a full step with fresh dropout
+masks and the scheduler's learning rate.
 """
 import argparse
 import json
