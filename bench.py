@@ -87,6 +87,20 @@ def parse():
     return ap.parse_args()
 
 
+# the engine captures the step after this many eager steps
+# (EagerEngine._fit_graphed(warmup=2)): the capture is the step after them
+GRAPH_EAGER_STEPS = 2
+
+
+def use_graph(flag, n, warmup):
+    """Whole-step HIP graph on one GPU (profiles/r4_g67: 6.7B -0.3 to -2.9 ms,
+    1.3B -1.3 ms, 345M as before), only when the warmup covers the capture
+    step so it never lands inside the timed region; ``flag`` >= 0 forces it."""
+    if flag >= 0:
+        return int(flag)
+    return int(n == 1 and warmup >= GRAPH_EAGER_STEPS + 1)
+
+
 def main():
     args = parse()
     import torch
@@ -150,10 +164,7 @@ def main():
     # as the reference's fp16 O2 gradients do -- half the reduce-scatter bytes
     grad_wire = args.grad_reduce_dtype or ("bfloat16" if n > 1 else "float32")
     ov.append("Distributed.comm.reduce_dtype=%s" % grad_wire)
-    # single GPU: the whole step as one HIP graph (profiles/r4_g67: 6.7B -0.8 ms,
-    # 1.3B -1.3 ms, 345M as before); captured after 2 eager steps, so only when
-    # the warmup covers the capture (never inside the timed region)
-    graph = args.hip_graph if args.hip_graph >= 0 else int(n == 1 and args.warmup >= 3)
+    graph = use_graph(args.hip_graph, n, args.warmup)
     ov.append("Engine.cuda_graph=%s" % bool(graph))
     # A/B experiments: extra config overrides, e.g. "Distributed.comm.early_grad_norm=False"
     ov += [o for o in os.environ.get("FLEETX_BENCH_OVERRIDES", "").split(";") if o]

@@ -67,3 +67,21 @@ def test_child_env_contract():
     assert env["PADDLE_TRAINER_ID"] == "3" and env["PADDLE_RANK_IN_NODE"] == "1"
     assert env["FLAGS_selected_gpus"] == "5" and env["HIP_VISIBLE_DEVICES"] == "4,5"
     assert env["FLEETX_RESTART_COUNT"] == "2" and env["MASTER_PORT"] == "6000"
+
+
+def test_bench_graph_capture_stays_in_warmup():
+    """bench.py's whole-step graph: on by default for one GPU only when the
+    warmup covers the capture step (the engine runs GRAPH_EAGER_STEPS eager
+    steps, then captures), so a capture never lands in the timed region;
+    multi-rank runs stay eager; --hip-graph forces either way."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from fleetx_amd.core.engine.eager_engine import EagerEngine
+    import inspect
+    eager = inspect.signature(EagerEngine._fit_graphed).parameters["warmup"].default
+    assert bench.GRAPH_EAGER_STEPS == eager
+    assert bench.use_graph(-1, 1, eager + 1) == 1
+    assert bench.use_graph(-1, 1, eager) == 0
+    assert bench.use_graph(-1, 2, 10) == 0
+    assert bench.use_graph(0, 1, 10) == 0
+    assert bench.use_graph(1, 1, 0) == 1
