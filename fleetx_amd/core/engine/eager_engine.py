@@ -359,7 +359,7 @@ class EagerEngine(BasicEngine):
         stream, under this step's forward."""
         defer = self._defer_update()
         if defer:
-            self.optimizer.launch_pending()
+            self.optimizer.launch_pending(capturing=torch.cuda.is_current_stream_capturing())
         self._graph_salt.add_(1)
         model = self._module.model
         model.train()
@@ -695,6 +695,11 @@ class EagerEngine(BasicEngine):
             self.optimizer.sync_state()  # an overlapped update may still be in flight
         if hasattr(self.buffer, "sync_params"):
             self.buffer.sync_params()  # and overlapped parameter gathers
+        if torch.cuda.is_available():
+            # never checkpoint the skipped / diverged state a timed-out one-shot
+            # all-reduce leaves behind: raise first, naming the group
+            torch.cuda.synchronize()
+            _comm.check_all()
         target = self._shard_dir(ckpt.step_dir(self._output_dir, epoch, step))
         # stage 3: gather full parameters first (reference get_all_parameters, :600-601)
         with self._params_gathered():

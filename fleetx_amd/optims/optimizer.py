@@ -136,10 +136,13 @@ class FlatOptimizer:
 
         A timed-out one-shot all-reduce (``parallel/comm.py``) counts as an
         overflow: with a norm, +inf joins the local sum of squares before the
-        shard / mp / pp reductions, so every rank of the check group skips the
-        step together; without one, the local flag is the found-inf."""
+        shard / mp / pp reductions; without one, the flag is the found-inf.
+        The flag is MAX-reduced over the world first, so every rank skips."""
         from ..parallel import comm as _comm
-        err = _comm.error_flag()
+        # a timeout is rank-local: shared with EVERY rank (MAX over the world)
+        # so all ranks skip the step together instead of the ranks that did
+        # not time out applying it alone
+        err = _comm.world_error_flag()
         need_norm = self.grad_clip is not None or self.loss_scale is not None
         if not need_norm:
             self.gscale.fill_(1.0)
@@ -183,11 +186,21 @@ class FlatOptimizer:
     defer_update = False
     _pending = None
 
-    def launch_pending(self):
-        """Deferred mode: start the previous step's update on the side stream."""
+    def launch_pending(self, capturing=False):
+        """Deferred mode: start the previous step's update on the side stream.
+
+        ``capturing``: the call is being recorded into the whole-step graph,
+        whose replays must ALWAYS hold the update launch -- even when a flush
+        (``sync_state``: eval / save / predict) cleared ``_pending`` between
+        the last eager call and the capture.  The launch reads its learning
+        rate from the device buffer of the graph and, after a flush, the
+        found-inf flag the flush raised, so the replay right after the capture
+        is a no-op update and every later replay applies its step's update."""
         if self._pending is not None:
             lr, self._pending = self._pending, None
             self._update_overlapped(lr)
+        elif capturing and self._overlap_groups is not None:
+            self._update_overlapped(self.get_lr())
 
     # ------------------------------------------------------------------ overlap
     _overlap_groups = None

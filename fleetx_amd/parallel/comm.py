@@ -217,7 +217,11 @@ class Communicator:
         # several ranks on one device, where RCCL refuses to run)
         nccl = dist.get_backend(group.group if group is not None else None) == "nccl"
         force = os.environ.get("FLEETX_ONESHOT_FORCE", "0") == "1"
-        if oneshot and self.nranks > 1 and torch.cuda.is_available() and (nccl or force):
+        # the same on every rank (env, backend, group size): world_error_flag
+        # keys its world collective on it
+        self.tried_oneshot = bool(oneshot and self.nranks > 1 and torch.cuda.is_available()
+                                  and (nccl or force))
+        if self.tried_oneshot:
             try:
                 self.oneshot = IpcAllReduce(group, max_bytes)
             except (RuntimeError, ValueError) as e:  # multi-node group, IPC refused, ...
@@ -274,6 +278,25 @@ def error_flag():
     for f in flags[1:]:
         out = out + f
     return out
+
+
+def world_error_flag():
+    """:func:`error_flag` shared by EVERY rank (MAX over the world, 4 bytes),
+    or :func:`error_flag` alone when no communicator attempted the one-shot
+    path.  Communicators are created by the same SPMD code on every rank and
+    the attempt depends only on env / backend / group size, so whether the
+    collective runs is the same everywhere, even where a group's one-shot
+    setup failed (that rank then contributes a zero)."""
+    err = error_flag()
+    if not any(c.tried_oneshot for c in _COMMS.values()):
+        return err
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return err
+    dev = torch.device("cuda", torch.cuda.current_device())
+    err = torch.zeros(1, dtype=torch.int32, device=dev) if err is None \
+        else (err != 0).to(torch.int32)
+    dist.all_reduce(err, op=dist.ReduceOp.MAX)
+    return err
 
 
 def reset():

@@ -37,6 +37,11 @@ _HCG = None
 #  * pp (activation p2p) and the tied-embedding pair: medium;
 #  * check (norm / found-inf scalars): latency-bound -> few.
 # ``(min_ctas, max_ctas)``; ``None`` leaves the bound to RCCL.
+# OPT-IN (``Distributed.comm.ctas: preset`` or a dict of overrides): the
+# budgets have not been measured on a multi-GPU xGMI node yet, and a data-group
+# cap of 16 channels could leave links of the 7-link mesh idle, so by default
+# no group carries options and the process-wide ``NCCL_MIN_NCHANNELS=32``
+# floor (utils/env.py) applies to every communicator.
 CTA_KEYS = {"dp": "data", "mp": "model", "pp": "pipe", "sharding": "sharding",
             "data_world": "data_world", "check": "check", "embedding": "embedding"}
 DEFAULT_CTAS = {"model": (32, 64), "data": (8, 16), "sharding": (8, 16),
@@ -56,11 +61,17 @@ def model_ctas(t):
 
 
 def parse_ctas(cfg):
-    """``Distributed.comm.ctas`` -> ``{group name: (min, max)}`` over the
-    defaults.  Values: ``"min,max"``, ``[min, max]`` or an int (max only);
-    ``None`` / ``False`` for a key drops the bound; ``ctas: False`` drops all."""
-    if cfg is False:
+    """``Distributed.comm.ctas`` -> ``{group name: (min, max)}``.
+
+    ``None`` / ``{}`` / ``False``: no per-group budget (RCCL's own choice over
+    the process-wide channel floor).  ``"preset"`` / ``True``: the
+    DEFAULT_CTAS table.  A dict: the table with these overrides -- values
+    ``"min,max"``, ``[min, max]`` or an int (max only); ``None`` / ``False``
+    for a key drops that group's bound."""
+    if cfg is False or cfg is None or (isinstance(cfg, dict) and not cfg):
         return {}
+    if cfg is True or cfg == "preset":
+        cfg = {}
     out = dict(DEFAULT_CTAS)
     for k, v in dict(cfg or {}).items():
         name = CTA_KEYS.get(k, k)
@@ -176,7 +187,8 @@ class HybridCommunicateGroup:
         self.stage_id = self.pp_rank
         self._nccl = self.initialized and dist.get_backend() == "nccl"
         self.ctas = parse_ctas(ctas) if ctas is not False else {}
-        self._model_ctas_set = bool(ctas) and any(CTA_KEYS.get(k, k) == "model" for k in ctas)
+        self._model_ctas_set = isinstance(ctas, dict) and any(CTA_KEYS.get(k, k) == "model"
+                                                              for k in ctas)
 
         self._groups = {}
         for axis in HybridTopology.AXES:

@@ -26,13 +26,13 @@ def get_world_size():
 
 
 # Process-wide RCCL environment (Distributed.comm.rccl_env; the process
-# environment always wins).  Empty by default: the channel (CTA) budget is
-# set PER COMMUNICATOR from Distributed.comm.ctas (parallel/topology.py
-# DEFAULT_CTAS) -- TP groups get many channels, gradient-bucket groups that
-# overlap backward GEMMs a capped number, scalar groups few -- instead of one
-# NCCL_MIN_NCHANNELS for every group.  tools/bench_collectives.py takes the
-# same keys.
-DEFAULT_RCCL_ENV = {}
+# environment always wins).  An 8-GPU MI355X node is a fully connected xGMI
+# mesh (7 point-to-point links per GPU): a bandwidth-optimal collective needs
+# enough channels that every link carries one, so the channel floor is
+# raised to 32 for every communicator.  Per-communicator budgets
+# (Distributed.comm.ctas, parallel/topology.py DEFAULT_CTAS) are opt-in until
+# tools/bench_collectives.py --ctas has measured them on a node.
+DEFAULT_RCCL_ENV = {"NCCL_MIN_NCHANNELS": "32"}
 
 
 def apply_rccl_env(config=None):

@@ -12,7 +12,9 @@ from tests import dist_utils
 
 
 def test_parse_defaults_and_overrides():
-    d = topo.parse_ctas(None)
+    assert topo.parse_ctas(None) == {} and topo.parse_ctas({}) == {}   # opt-in
+    d = topo.parse_ctas("preset")
+    assert d == topo.parse_ctas(True)
     assert d["model"] == (32, 64) and d["data"] == (8, 16) and d["check"] == (1, 4)
     assert d["pipe_bwd"] == d["pipe"]
     o = topo.parse_ctas({"dp": "4,8", "mp": 48, "pp": [2, 4], "check": None})
@@ -71,3 +73,12 @@ def test_model_budget_scales_with_group_size():
     assert topo.model_ctas(2) == (8, 16)
     assert topo.model_ctas(4) == (16, 32)
     assert topo.model_ctas(8) == topo.DEFAULT_CTAS["model"] == (32, 64)
+
+
+def test_default_topology_sets_no_group_budget():
+    """Budgets are opt-in: without ``Distributed.comm.ctas`` no group carries
+    options (the process-wide NCCL_MIN_NCHANNELS floor applies)."""
+    res = dist_utils.run(_build, 8, None)
+    assert all(lo is None and hi is None for _, lo, hi in res[0]["seen"])
+    from fleetx_amd.utils import env
+    assert env.DEFAULT_RCCL_ENV.get("NCCL_MIN_NCHANNELS") == "32"

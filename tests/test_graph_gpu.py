@@ -146,3 +146,29 @@ def test_graph_with_deferred_overlapped_update_matches_serial(monkeypatch):
         assert torch.equal(a, b), n
     assert any(not torch.equal(mid[n], p) for n, p in eng._module.model.named_parameters())
     assert all(l == l for l in losses)
+
+
+def test_graph_flush_before_capture_keeps_update_in_graph(monkeypatch):
+    """A flush (sync_state: eval / save) between the last eager warmup call and
+    the capture clears the host's pending update; the captured body must still
+    hold the update launch, or every replay would silently skip its AdamW.
+    Bitwise against the serial-update graph."""
+    monkeypatch.setenv("FLEETX_DETERMINISTIC", "1")
+    bs = _batches(6)
+    ser = _engine(True, 0.0, extra=["Distributed.comm.overlap_optimizer=False"])
+    _run(ser, bs)
+    ser.optimizer.sync_state()
+    torch.cuda.synchronize()
+    eng = _engine(True, 0.0)
+    assert eng.optimizer.defer_update and eng._cuda_graph
+    _run(eng, bs[:2])                   # the two eager warmup calls
+    eng.optimizer.sync_state()          # flush right before the capture call
+    assert eng.optimizer._pending is None
+    _run(eng, bs[2:])                   # capture + replays
+    assert eng._graph is not None
+    eng.optimizer.sync_state()
+    torch.cuda.synchronize()
+    assert int(eng.optimizer.dev_step.item()) == 6
+    for (n, a), (_, b) in zip(ser._module.model.named_parameters(),
+                              eng._module.model.named_parameters()):
+        assert torch.equal(a, b), n

@@ -49,7 +49,7 @@ def cta_budget(spec):
     if spec in (None, "", "none"):
         return None
     if spec in topo.CTA_KEYS:
-        return topo.parse_ctas(None).get(topo.CTA_KEYS[spec])
+        return topo.parse_ctas("preset").get(topo.CTA_KEYS[spec])
     return topo.parse_ctas({"dp": spec})["data"]
 
 
