@@ -31,6 +31,7 @@
 int fx_gemm5_launch(int dt, int la, int lb, int epi, const fxg::GemmParams& P, hipStream_t st);
 long fx_gemm5_ws_bytes(int M, int N, int K);
 void fx_gemm5_set_geom(int nf, int split);
+void fx_gemm5_set_persist(int on);
 
 using namespace fxg;
 
@@ -140,9 +141,25 @@ extern "C" int fx_gemm(int dt, int la, int lb, int epi, int M, int N, int K, con
 // Tile-order M-group height (tools/bench_gemm.py --gm sweeps; 0 = tuned / default).
 extern "C" void fx_gemm_set_gm(int gm) { g_gm = gm > 0 ? gm : 0; }
 
+// Shipped plan (fleetx_amd/ops/gemm_plan_gfx950.json, tools/gemm_plan.py):
+// preload the tile order of a shape so its first call neither times
+// candidates nor depends on box noise; a shape that is in the table is never
+// re-tuned.
+extern "C" void fx_gemm_set_tuned(int la, int lb, int f32, int M, int N, int K, int gm) {
+  g_gm_tuned[std::make_tuple(la, lb, f32, M, N, K)] = gm;
+}
+
+// 0: no first-call tuning (shapes missing from the plan run gm 8:
+// FLEETX_DETERMINISTIC); 1: tune them.  < 0 re-reads FLEETX_GEMM_TUNE.
+extern "C" void fx_gemm_set_tune(int on) { g_tune = on; }
+
 // Lab override of the tile geometry (4 / 8) and split-K slices (1 = none);
 // 0 = the shape's plan.
 extern "C" void fx_gemm_set_geom(int nf, int split) { fx_gemm5_set_geom(nf, split); }
+
+// Persistent 16-bit launches on (1) / off (0, one workgroup per tile) for
+// A/B runs and the bitwise test; < 0 = FLEETX_GEMM5_PERSIST.
+extern "C" void fx_gemm_set_persist(int on) { fx_gemm5_set_persist(on); }
 
 // The tuned table: (la, lb, fp32 out, M, N, K, gm) rows, flattened.
 extern "C" int fx_gemm_tuned(long* out, int cap) {

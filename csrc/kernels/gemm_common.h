@@ -37,6 +37,11 @@ struct GemmParams {
   int tile0;
   int ksplit;
   float* ws;
+  // persistent launch (gemm5, 16-bit outputs): gridDim.x resident workgroups
+  // pull tiles from the 8 per-XCD queues of ring slot `qslot` (int 32 x for
+  // XCD x, int 256 the finish count; the last workgroup to finish re-zeroes
+  // the slot); -1 = one workgroup per tile
+  int qslot;
 };
 
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {

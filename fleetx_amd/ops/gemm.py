@@ -127,11 +127,102 @@ TUNE_KINDS = ("dgrad",)
 ROUTE_MARGIN = 0.03
 VENDOR = {}
 _ROUTE = {}
+_ROUTE_SRC = {}  # key -> "plan" | "race" | "default"
+PLAN_KINDS = ("fwd", "fwd_act", "dgrad", "dgrad_act", "wgrad")
+
+# ----------------------------------------------------------------------------
+# Shipped GEMM plan (reproducible routing; reference parity: the fused path is
+# chosen at config time, ``models/language_model/utils.py:30-36,67-71``).
+# ``gemm_plan_gfx950.json`` (tools/gemm_plan.py: many interleaved launches per
+# candidate on an MI355X) holds, per (kind, dtype, M, N, K) of the model zoo's
+# layer shapes, the route (MFMA kernel or vendor) and the tile-order M-group
+# height.  Shapes in the plan are never raced or re-tuned, so one tree runs the
+# same kernels with the same tile orders on every box and under a profiler;
+# the first-call race / tune remains only for shapes the plan lacks, and not
+# at all under FLEETX_DETERMINISTIC=1 (missing shapes: vendor path, gm 8).
+# Key convention: M = rows of the activation (tokens), N = output columns,
+# K = reduction; wgrad: M = tokens, N = out features, K = in features.
+# ----------------------------------------------------------------------------
+PLAN_FILE = os.environ.get("FLEETX_GEMM_PLAN",
+                           os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                        "gemm_plan_gfx950.json"))
+_PLAN = None  # {(kind, dtype, M, N, K): entry}
+
+
+def _deterministic():
+    return os.environ.get("FLEETX_DETERMINISTIC", "0") == "1"
+
+
+_KIND_LAYOUT = {"fwd": (LAY_KC, LAY_KC, 0), "fwd_act": (LAY_KC, LAY_KC, 0),
+                "dgrad": (LAY_KC, LAY_MC, 0), "dgrad_act": (LAY_KC, LAY_MC, 0),
+                "wgrad": (LAY_MC, LAY_MC, 1)}
+
+
+def kernel_shape(kind, M, N, K):
+    """(la, lb, fp32 out, M, N, K) of the kernel launch for a plan key."""
+    la, lb, f32 = _KIND_LAYOUT[kind]
+    if kind == "wgrad":
+        return la, lb, f32, N, K, M
+    return la, lb, f32, M, N, K
+
+
+def load_plan(path=None, force=False):
+    """Read the plan (once) and preload its tile orders into the kernel
+    library; returns {key: entry}.  A missing / foreign-arch plan is empty."""
+    global _PLAN
+    if _PLAN is not None and not force:
+        return _PLAN
+    import json
+    plan = {}
+    path = path or PLAN_FILE
+    try:
+        with open(path) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        doc = {}
+    arch = doc.get("arch", "gfx950")
+    ok_arch = True
+    if torch.cuda.is_available():
+        name = getattr(torch.cuda.get_device_properties(0), "gcnArchName", "") or ""
+        ok_arch = not name or name.split(":")[0] == arch
+    if ok_arch:
+        for e in doc.get("entries", []):
+            key = (e["kind"], e.get("dtype", "bf16"), int(e["M"]), int(e["N"]), int(e["K"]))
+            plan[key] = e
+    _PLAN = plan
+    if plan and _lib.available() and torch.cuda.is_available():
+        k = _lib.kernels()
+        for (kind, dt, M, N, K), e in plan.items():
+            if e.get("gm"):
+                k.gemm_set_tuned(*kernel_shape(kind, M, N, K), int(e["gm"]))
+    if _deterministic() and _lib.available():
+        _lib.kernels().gemm_set_tune(0)
+    return plan
+
+
+def _dt_name(dtype):
+    return "bf16" if dtype == torch.bfloat16 else "fp16"
+
+
+def plan_route(kind, M, N, K, dtype):
+    """True / False when the plan fixes the route of this shape, else None."""
+    e = load_plan().get((kind, _dt_name(dtype), M, N, K))
+    if e is None or "route" not in e:
+        return None
+    return e["route"] == "kernel"
 
 
 def route_table():
     """{(kind, M, N, K): True if the MFMA kernel takes it} decided so far."""
     return {k[:4]: v for k, v in _ROUTE.items()}
+
+
+def route_sources():
+    """{"plan": n, "race": n, "default": n}: where the routes came from."""
+    out = {"plan": 0, "race": 0, "default": 0}
+    for v in _ROUTE_SRC.values():
+        out[v] += 1
+    return out
 
 
 def _race(f_hip, f_vendor, iters=3):
@@ -162,8 +253,13 @@ def _tuned_route(kind, a, b):
     r = _ROUTE.get(key)
     if r is not None:
         return r
-    if out_tiles(kind, a, b) < MIN_TILES or kind not in VENDOR or not _ok(a2, b):
-        _ROUTE[key] = False
+    p = plan_route(kind, M, N, K, a.dtype)
+    if p is not None:
+        _ROUTE[key], _ROUTE_SRC[key] = p and _ok(a2, b), "plan"
+        return _ROUTE[key]
+    if out_tiles(kind, a, b) < MIN_TILES or kind not in VENDOR or not _ok(a2, b) \
+            or _deterministic():
+        _ROUTE[key], _ROUTE_SRC[key] = False, "default"
         return False
     if torch.cuda.is_current_stream_capturing():
         return False
@@ -171,7 +267,7 @@ def _tuned_route(kind, a, b):
         r = _race(lambda: linear_fwd(a2, b), lambda: VENDOR["fwd"](a2, b))
     else:
         r = _race(lambda: linear_dgrad(a2, b), lambda: VENDOR["dgrad"](a2, b))
-    _ROUTE[key] = r
+    _ROUTE[key], _ROUTE_SRC[key] = r, "race"
     return r
 
 
@@ -184,6 +280,8 @@ def use(kind, a, b=None):
     if _MODE == "auto":
         if b is None:
             return False
+        if kind in PLAN_KINDS and (kind in TUNE_KINDS or kind in AUTO_KINDS):
+            load_plan()
         if kind in AUTO_KINDS:
             return out_tiles(kind, a, b) >= (WGRAD_MIN_TILES if kind == "wgrad" else MIN_TILES)
         if ROUTE_TUNE and kind in TUNE_KINDS:

@@ -293,3 +293,82 @@ def test_wgrad_forced_geometry(gemm, nf, split):
     finally:
         k.gemm_set_geom(0, 0)
     assert _rel(out, base + dy.float().t() @ x.float()) < 1e-4
+
+
+# Persistent 16-bit launches (gemm5 ``P.qslot``): more tiles than resident
+# workgroups, pulled from per-XCD queues.  (4096, 6144, 256): 384 tiles of
+# 256 on 256 workgroups; (2560, 4608, 256): 720 tiles of 128 on 512.
+PERSIST_SHAPES = [(4096, 6144, 256), (2560, 4608, 256)]
+
+
+@pytest.fixture
+def persist_mode(gemm):
+    from fleetx_amd.ops import _lib
+    yield _lib.kernels().gemm_set_persist
+    _lib.kernels().gemm_set_persist(-1)
+
+
+@pytest.mark.parametrize("M,N,K", PERSIST_SHAPES)
+def test_persistent_matches_one_tile_per_workgroup(gemm, persist_mode, M, N, K):
+    """Every tile is computed exactly once whichever workgroup pulls it: the
+    persistent launch is bitwise the one-workgroup-per-tile launch, for the
+    forward (bias + GeLU epilogue too) and the data gradient."""
+    torch.manual_seed(6)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    w2 = torch.randn(N, 512, device="cuda", dtype=torch.bfloat16) * 0.05
+    outs = {}
+    for mode in (0, 1):
+        persist_mode(mode)
+        y = gemm.linear_fwd(x, w, b)
+        g, h = gemm.linear_fwd(x, w, b, act="gelu")
+        dx = gemm.linear_dgrad(dy, w2)
+        outs[mode] = (y, g, h, dx)
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)
+    ref = x.float() @ w.float().t() + b.float()
+    assert _rel(outs[1][0], ref) < 1e-2
+    assert _rel(outs[1][3], dy.float() @ w2.float()) < 1e-2
+
+
+def test_persistent_queue_slots_recycle(gemm, persist_mode):
+    """More launches than queue slots (4096): each launch re-zeroes its slot,
+    so a reused slot starts from an empty queue (a stale count would skip
+    tiles and leave the output partly unwritten)."""
+    persist_mode(1)
+    torch.manual_seed(7)
+    M, N, K = 2560, 4608, 128
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    ref = gemm.linear_fwd(x, w)
+    out = torch.empty_like(ref)
+    for i in range(4200):
+        if i % 700 == 0:
+            out.fill_(float("nan"))
+        gemm.linear_fwd(x, w, out=out)
+        if i % 700 == 699:
+            assert torch.equal(out, ref), i
+    torch.cuda.synchronize()
+
+
+def test_persistent_two_streams(gemm, persist_mode):
+    """Two persistent GEMMs in flight on two streams use different slots."""
+    persist_mode(1)
+    torch.manual_seed(8)
+    M, N, K = 4096, 6144, 256
+    xs = [torch.randn(M, K, device="cuda", dtype=torch.bfloat16) for _ in range(2)]
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    refs = [x.float() @ w.float().t() for x in xs]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    ys = [None, None]
+    for _ in range(20):
+        with torch.cuda.stream(s):
+            ys[1] = gemm.linear_fwd(xs[1], w)
+        ys[0] = gemm.linear_fwd(xs[0], w)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    for y, r in zip(ys, refs):
+        assert _rel(y, r) < 1e-2

@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--iters", type=int, default=12)
     ap.add_argument("--only", default="", help="comma list of shape names (qkv,out,fc1,fc2)")
     ap.add_argument("--paths", default="blas,hip", help="comma list of GEMM paths")
+    ap.add_argument("--chunks", type=int, default=1,
+                    help="split the update into this many launches (the step launches one "
+                         "per layer unit: ~66 at 6.7B)")
     a = ap.parse_args()
     from fleetx_amd.ops import _lib
     from fleetx_amd.ops import gemm as G
@@ -49,9 +52,13 @@ def main():
     side = torch.cuda.Stream()
 
     def adamw_once():
-        k.adamw_flat(0, master.data_ptr(), grad.data_ptr(), m1.data_ptr(), v1.data_ptr(),
-                     p16.data_ptr(), n, 1e-4, 0.9, 0.95, 1e-8, 0.01, 0.0, gs.data_ptr(),
-                     fi.data_ptr(), ds.data_ptr(), _lib.stream())
+        c = n // a.chunks
+        for i in range(a.chunks):
+            o = i * c
+            ln = n - o if i == a.chunks - 1 else c
+            k.adamw_flat(0, master[o:].data_ptr(), grad[o:].data_ptr(), m1[o:].data_ptr(),
+                         v1[o:].data_ptr(), p16[o:].data_ptr(), ln, 1e-4, 0.9, 0.95, 1e-8, 0.01,
+                         0.0, gs.data_ptr(), fi.data_ptr(), ds.data_ptr(), _lib.stream())
 
     shapes = {"qkv": (h, 3 * h), "out": (h, h), "fc1": (h, 4 * h), "fc2": (4 * h, h)}
     only = [s for s in a.only.split(",") if s]
@@ -69,7 +76,8 @@ def main():
     torch.cuda.synchronize()
     t_adam = e0.elapsed_time(e1)
     rows.append({"case": "adamw_alone", "ms": round(t_adam, 3),
-                 "TB_s": round(30.0 * n / t_adam / 1e9, 2), "grid": a.grid})
+                 "TB_s": round(30.0 * n / t_adam / 1e9, 2), "grid": a.grid,
+                 "chunks": a.chunks})
     print(json.dumps(rows[-1]), flush=True)
     for name, (K, N) in shapes.items():
         if only and name not in only:
