@@ -372,3 +372,34 @@ def test_persistent_two_streams(gemm, persist_mode):
     torch.cuda.synchronize()
     for y, r in zip(ys, refs):
         assert _rel(y, r) < 1e-2
+
+
+@pytest.mark.parametrize("act", [None, "gelu"])
+def test_persistent_under_memory_pressure(gemm, persist_mode, act):
+    """Persistent launches while another stream saturates HBM (as the
+    forward-overlapped AdamW does in the step): the next tile's K-tiles are
+    issued before the current tile's epilogue and MAIN waits for them with a
+    counted vmcnt; under long load latencies a wrong count reads stale LDS.
+    Bitwise against one-workgroup-per-tile, repeated."""
+    torch.manual_seed(9)
+    M, N, K = 8192, 6144, 4096
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    persist_mode(0)
+    ref = gemm.linear_fwd(x, w, b, act=act)
+    ref = ref if act is None else ref[0]
+    persist_mode(1)
+    big = torch.empty(1 << 29, device="cuda", dtype=torch.float32)  # 2 GiB
+    dst = torch.empty_like(big)
+    s = torch.cuda.Stream()
+    for _ in range(6):
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(4):
+                dst.copy_(big)
+        y = gemm.linear_fwd(x, w, b, act=act)
+        y = y if act is None else y[0]
+        torch.cuda.current_stream().wait_stream(s)
+        assert torch.equal(y, ref)
+    torch.cuda.synchronize()

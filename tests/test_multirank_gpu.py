@@ -118,6 +118,11 @@ def _master_norm(eng):
 def ref_gpu():
     r = dist_utils.run(_train_gpu, 1, (1, 1, 1, 1, 0, GBS, False, 1), timeout=300)
     assert r[0]["native"]
+    # bf16-noise scale per tensor: the same single-rank training with the batch
+    # split into 2 micro-batches (mathematically identical, different GEMM
+    # shapes and fp32 accumulation order)
+    n = dist_utils.run(_train_gpu, 1, (1, 1, 1, 1, 0, GBS // 2, False, 1), timeout=300)
+    r[0]["noise"] = {k: float((v - r[0]["master"][k]).norm()) for k, v in n[0]["master"].items()}
     return r[0]
 
 
@@ -141,12 +146,34 @@ def _check(results, ref_run):
         # fp32 master weights after the last update
         assert abs(r["pnorm"] - ref_run["pnorm"]) < 1e-3 * ref_run["pnorm"], \
             (r["pnorm"], ref_run["pnorm"])
-    # ... and tensor by tensor in the single-rank layout (bf16 compute: the
-    # per-tensor error is bounded by a fraction of the tensor's update: 10 % seen on
-    # zero-initialised biases, where Adam turns bf16 gradient noise into sign flips;
-    # a permuted or misplaced shard gives ~140 %)
-    from tests.test_distributed_cpu import check_master_per_tensor
-    check_master_per_tensor(results[0]["master"], ref_run["master"], ref_run["master0"], rel=0.3)
+    # ... and tensor by tensor in the single-rank layout, against the tensor's
+    # own bf16-noise scale (ref_gpu["noise"]: the single-rank run with another
+    # micro-batch split): err <= 3 x noise + 2 % of the tensor's update (+ a
+    # 1e-4 relative floor).  A permuted or misplaced shard gives ~140 % of the
+    # update; a 20 % gradient-scale error confined to one shard moves that
+    # shard's update by ~20 % -- both far outside the noise.
+    check_master_against_noise(results[0]["master"], ref_run)
+
+
+def check_master_against_noise(got, ref_run, k=3.0, rel=0.02):
+    ref, ref0, noise = ref_run["master"], ref_run["master0"], ref_run["noise"]
+    names = set(x.replace("#tied", "") for x in got)
+    assert names == set(ref), sorted(names ^ set(ref))
+    worst = (0.0, None)
+    from tests.test_distributed_cpu import _drop_key_bias
+    for name, w in got.items():
+        base = name.replace("#tied", "")
+        r, r0 = ref[base], ref0[base]
+        nz = noise[base]
+        if "qkv" in base and base.endswith("bias"):
+            w, r, r0 = (_drop_key_bias(x, 4) for x in (w, r, r0))
+        assert w.shape == r.shape, (name, w.shape, r.shape)
+        upd = float((r - r0).norm())
+        err = float((w - r).norm())
+        bound = k * nz + rel * upd + 1e-4 * float(r.norm())
+        worst = max(worst, (err / bound, name))
+        assert err <= bound, (name, err, nz, upd)
+    print("per-tensor worst err/bound: %.3f (%s)" % worst)
 
 
 LAYOUTS = {

@@ -31,6 +31,10 @@ def main():
     ap.add_argument("--iters", type=int, default=12)
     ap.add_argument("--only", default="", help="comma list of shape names (qkv,out,fc1,fc2)")
     ap.add_argument("--paths", default="blas,hip", help="comma list of GEMM paths")
+    ap.add_argument("--wide", type=int, default=0,
+                    help="1024-thread AdamW workgroups (16 waves: one workgroup per CU)")
+    ap.add_argument("--grid-sweep", default="",
+                    help="comma list of AdamW grids to time alone (e.g. 32,64,96,128) and exit")
     ap.add_argument("--chunks", type=int, default=1,
                     help="split the update into this many launches (the step launches one "
                          "per layer unit: ~66 at 6.7B)")
@@ -63,10 +67,26 @@ def main():
     shapes = {"qkv": (h, 3 * h), "out": (h, h), "fc1": (h, 4 * h), "fc2": (4 * h, h)}
     only = [s for s in a.only.split(",") if s]
     rows = []
+    if a.grid_sweep:
+        # AdamW alone on a limited number of workgroups: how many CUs the
+        # update needs to stream at HBM rate
+        for g in [int(x) for x in a.grid_sweep.split(",")]:
+            k.adamw_tune(g, 1, a.wide)
+            adamw_once()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            adamw_once()
+            e1.record()
+            torch.cuda.synchronize()
+            t = e0.elapsed_time(e1)
+            print(json.dumps({"case": "adamw_grid", "grid": g, "wide": a.wide, "ms": round(t, 3),
+                              "TB_s": round(30.0 * n / t / 1e9, 2)}), flush=True)
+        return
     # AdamW alone (rate)
     with torch.cuda.stream(side):
         if a.grid:
-            k.adamw_tune(a.grid, 1, 0)
+            k.adamw_tune(a.grid, 1, a.wide)
         adamw_once()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

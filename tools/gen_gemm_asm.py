@@ -288,6 +288,21 @@ def body_with(st, la, lb, dt, kind, read_gap, dma_gap):
     return st.lines, st.pending
 
 
+def split_pre_main(lines):
+    """Split a generated stream for the persistent kernel: PRE = the prologue's
+    LDS-DMA issue of K-tiles 0 and 1 (issued for the NEXT output tile before
+    the current tile's epilogue, so its load latency hides under the epilogue),
+    MAIN = the rest, whose first wait counts the epilogue's stores issued in
+    between (``%[pw]``: 2 nf loads of K-tile 1 + the stores, capped at 63)."""
+    nf = GEO["nf"]
+    first_wait = "s_waitcnt vmcnt(%d)" % (2 * nf)
+    idx = lines.index(first_wait)
+    assert lines[0] == "s_mov_b32 %[keep], m0"
+    pre = lines[:idx] + ["s_mov_b32 m0, %[keep]"]
+    main = ["s_mov_b32 %[keep], m0", "s_waitcnt vmcnt(%[pw])"] + lines[idx + 1:]
+    return pre, main
+
+
 def c_string(lines):
     return "\n".join('  "%s\\n"' % l for l in lines)
 
@@ -339,6 +354,16 @@ def main():
                 parts.append("#define FX_G5_%s_%s_%s_%s \\\n%s\n" % (
                     tag, names[la], names[lb], dt.upper(),
                     " \\\n".join('  "%s\\n"' % l for l in lines)))
+                if la == MC and lb == MC:
+                    continue  # weight gradients (fp32 out) are not persistent
+                pre, main = split_pre_main(lines)
+                if dt == "bf16":  # the DMA prologue is the same for both dtypes
+                    parts.append("#define FX_G5_%s_%s_%s_PRE \\\n%s\n" % (
+                        tag, names[la], names[lb],
+                        " \\\n".join('  "%s\\n"' % l for l in pre)))
+                parts.append("#define FX_G5_%s_%s_%s_%s_MAIN \\\n%s\n" % (
+                    tag, names[la], names[lb], dt.upper(),
+                    " \\\n".join('  "%s\\n"' % l for l in main)))
     with open(path, "w") as f:
         f.write("\n".join(parts))
     print("wrote", os.path.normpath(path), file=sys.stderr)
