@@ -44,6 +44,9 @@ void fx_sumsq_chunks(const int64_t*, const int64_t*, int, float*, hipStream_t);
 void fx_adamw_tune(int, int, int);
 void fx_adamw_flat(int, float*, const float*, float*, float*, void*, long, float, float, float,
                    float, float, float, const float*, const int*, const int*, hipStream_t);
+void fx_adamw_flat_g16(int, float*, const void*, float*, float*, void*, long, float, float,
+                       float, float, float, float, const float*, const int*, const int*,
+                       hipStream_t);
 void fx_cast_f32(int, const float*, void*, long, hipStream_t);
 void fx_accum_f32(int, float*, const void*, long, int, hipStream_t);
 void fx_embedding_fwd(int, const int64_t*, const int64_t*, const void*, const void*, void*, int,
@@ -213,6 +216,13 @@ PYBIND11_MODULE(_kernels, m) {
                          ptr step, ptr st) {
     fx_adamw_flat(dt, F(p), F(g), F(mm), F(vv), P(p16), n, lr, b1, b2, eps, wd, l2, F(gscale),
                   reinterpret_cast<const int*>(skip), reinterpret_cast<const int*>(step), S(st));
+  });
+  m.def("adamw_flat_g16", [](int dt, ptr p, ptr g, ptr mm, ptr vv, ptr p16, long n, float lr,
+                             float b1, float b2, float eps, float wd, float l2, ptr gscale,
+                             ptr skip, ptr step, ptr st) {
+    fx_adamw_flat_g16(dt, F(p), CP(g), F(mm), F(vv), P(p16), n, lr, b1, b2, eps, wd, l2,
+                      F(gscale), reinterpret_cast<const int*>(skip),
+                      reinterpret_cast<const int*>(step), S(st));
   });
   m.def("cast_f32", [](int dt, ptr x, ptr y, long n, ptr st) {
     fx_cast_f32(dt, F(x), P(y), n, S(st));

@@ -53,7 +53,7 @@ static std::map<std::tuple<int, int, int, int, int, int>, int> g_gm_tuned;
 static const int kGmCand[] = {1, 2, 4, 8, 16};
 
 static int gemm_tuned_gm(int dt, int la, int lb, int epi, const GemmParams& P0, hipStream_t st) {
-  const int f32 = epi == EPI_F32;
+  const int f32 = epi_wgrad(epi);
   const auto key = std::make_tuple(la, lb, f32, P0.M, P0.N, P0.K);
   auto it = g_gm_tuned.find(key);
   if (it != g_gm_tuned.end()) return it->second;
@@ -107,7 +107,8 @@ extern "C" int fx_gemm(int dt, int la, int lb, int epi, int M, int N, int K, con
                        long lda, const void* B, long ldb, void* C, long ldc, const void* bias,
                        void* aux, long ldaux, int beta, hipStream_t st, float* sq, float* ws) {
   if (M <= 0 || N <= 0 || K < 2 * BK || K % BK) return -1;
-  if (sq != nullptr && epi != EPI_F32) return -5;
+  if (sq != nullptr && !epi_wgrad(epi)) return -5;
+  if (epi == EPI_F32B && beta) return -6;  // 16-bit gradients are written, never accumulated
   if (N % 4 || (la == LAY_MC && M % 8) || (lb == LAY_MC && N % 8)) return -2;
   if (M < 8 || N < 8) return -2;
   const long a_span = la == LAY_KC ? (long)M * lda : (long)BK * lda + M;
@@ -125,7 +126,7 @@ extern "C" int fx_gemm(int dt, int la, int lb, int epi, int M, int N, int K, con
   P.M = M; P.N = N; P.K = K;
   P.beta = beta;
   P.sq = sq;
-  P.ws = epi == EPI_F32 ? ws : nullptr;
+  P.ws = epi_wgrad(epi) ? ws : nullptr;
   if (g_gm < 0) {
     const char* e = getenv("FLEETX_GEMM_GM");
     g_gm = e ? atoi(e) : 0;
@@ -177,6 +178,6 @@ extern "C" int fx_gemm_tuned(long* out, int cap) {
 // Split-K workspace (bytes) fx_gemm wants in `ws` for an fp32 weight-gradient
 // GEMM of this shape; 0 = it runs unsplit (gemm5.hip g5_split_plan).
 extern "C" long fx_gemm_ws_bytes(int epi, int M, int N, int K) {
-  if (epi != EPI_F32 || K < 2 * BK || K % BK) return 0;
+  if (!epi_wgrad(epi) || K < 2 * BK || K % BK) return 0;
   return fx_gemm5_ws_bytes(M, N, K);
 }

@@ -8,7 +8,13 @@ namespace fxg {
 
 enum { LAY_KC = 0, LAY_MC = 1 };
 enum { EPI_STORE = 0, EPI_BIAS_GELU = 1, EPI_DGELU = 2, EPI_F32 = 3, EPI_BIAS_GELU_ERF = 4,
-       EPI_DGELU_ERF = 5 };
+       EPI_DGELU_ERF = 5,
+       // weight gradient stored in 16 bits (fp32 accumulation, beta 0): the
+       // bf16 gradient storage of Distributed.comm.grad_dtype
+       EPI_F32B = 6 };
+
+// the fp32-accumulating weight-gradient epilogues (split-K, norm partials)
+constexpr bool epi_wgrad(int e) { return e == EPI_F32 || e == EPI_F32B; }
 
 constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int PIECE = 16384;            // bytes per staged piece (128 rows x 64 k x 2 B)
@@ -42,6 +48,9 @@ struct GemmParams {
   // XCD x, int 256 the finish count; the last workgroup to finish re-zeroes
   // the slot); -1 = one workgroup per tile
   int qslot;
+  // EPI_F32B: 1 = this launch stores the 16-bit gradient, 0 = fp32 split-K
+  // partial slabs (the combine stores the 16-bit result)
+  int out16;
 };
 
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {

@@ -189,9 +189,29 @@ __device__ __forceinline__ void st_stream(V x, V* a, bool nt) {
 // forward-overlapped update runs (1024, 4) on a capped grid instead: few CUs,
 // each with 256 KiB of loads in flight, so the GEMMs beside it keep the rest
 // of the chip (optims/optimizer.py, _update_overlapped).
-template <typename T, bool NT, int BS, int U>
+// G16: the gradient is stored in the model's 16-bit dtype (the bf16
+// gradient storage of Distributed.comm.grad_dtype: 2 B read per parameter
+// instead of 4 -- 28 instead of 30 B per parameter per step)
+template <typename T, bool G16>
+__device__ __forceinline__ floatx4 adamw_ld_grad(const void* g, long i, bool nt) {
+  if constexpr (G16) {
+    const unsigned long long h = ld_stream(reinterpret_cast<const unsigned long long*>(g) + i, nt);
+    return floatx4{Elt<T>::to_f((uint16_t)h), Elt<T>::to_f((uint16_t)(h >> 16)),
+                   Elt<T>::to_f((uint16_t)(h >> 32)), Elt<T>::to_f((uint16_t)(h >> 48))};
+  } else {
+    return ld_stream(reinterpret_cast<const floatx4*>(g) + i, nt);
+  }
+}
+
+template <typename T, bool G16>
+__device__ __forceinline__ float adamw_grad1(const void* g, long i) {
+  if constexpr (G16) return Elt<T>::to_f(reinterpret_cast<const uint16_t*>(g)[i]);
+  else return reinterpret_cast<const float*>(g)[i];
+}
+
+template <typename T, bool NT, int BS, int U, bool G16 = false>
 __global__ __launch_bounds__(BS) void adamw_flat_kernel(
-    float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+    float* __restrict__ p, const void* __restrict__ g, float* __restrict__ m,
     float* __restrict__ v, uint16_t* __restrict__ p16, long n, float lr, float beta1,
     float beta2, float eps, float wd, float l2, const float* __restrict__ gscale,
     const int* __restrict__ skip, const int* __restrict__ step, const float* __restrict__ lr_dev) {
@@ -213,7 +233,7 @@ __global__ __launch_bounds__(BS) void adamw_flat_kernel(
       const long i = i0 + (long)u * BS;
       if (i < n4) {
         pp[u] = ld_stream(reinterpret_cast<const floatx4*>(p) + i, NT);
-        gg[u] = ld_stream(reinterpret_cast<const floatx4*>(g) + i, NT);
+        gg[u] = adamw_ld_grad<T, G16>(g, i, NT);
         mm[u] = ld_stream(reinterpret_cast<const floatx4*>(m) + i, NT);
         vv[u] = ld_stream(reinterpret_cast<const floatx4*>(v) + i, NT);
       }
@@ -246,7 +266,7 @@ __global__ __launch_bounds__(BS) void adamw_flat_kernel(
     }
   }
   for (long i = n4 * 4 + blockIdx.x * (long)BS + threadIdx.x; i < n; i += (long)gridDim.x * BS) {
-    const float gr = g[i] * gs + l2 * p[i];
+    const float gr = adamw_grad1<T, G16>(g, i) * gs + l2 * p[i];
     m[i] = beta1 * m[i] + (1.f - beta1) * gr;
     v[i] = beta2 * v[i] + (1.f - beta2) * gr * gr;
     const float denom = sqrtf(v[i]) * inv_sqrt_bc2 + eps;
@@ -412,8 +432,8 @@ extern "C" void fx_adamw_tune(int grid, int nt, int wide) {
   g_adamw_wide = wide;
 }
 
-template <typename T, bool NT, int BS, int U>
-static void adamw_launch(float* p, const float* g, float* m, float* v, void* p16, long n,
+template <typename T, bool NT, int BS, int U, bool G16 = false>
+static void adamw_launch(float* p, const void* g, float* m, float* v, void* p16, long n,
                          float lr, float beta1, float beta2, float eps, float wd, float l2,
                          const float* gscale, const int* skip, const int* step, hipStream_t st) {
   // at most 8 resident 256-thread blocks per CU (2 of 1024)
@@ -422,7 +442,7 @@ static void adamw_launch(float* p, const float* g, float* m, float* v, void* p16
   const long cap = 256L * (8 * 256 / BS) * 4;
   int grid = (int)(blocks < 1 ? 1 : (blocks > cap ? cap : blocks));
   if (g_adamw_grid > 0 && g_adamw_grid < grid) grid = g_adamw_grid;
-  adamw_flat_kernel<T, NT, BS, U><<<grid, BS, 0, st>>>(p, g, m, v, (uint16_t*)p16, n, lr, beta1,
+  adamw_flat_kernel<T, NT, BS, U, G16><<<grid, BS, 0, st>>>(p, g, m, v, (uint16_t*)p16, n, lr, beta1,
                                                       beta2, eps, wd, l2, gscale, skip, step,
                                                       g_adamw_lr);
 }
@@ -438,6 +458,22 @@ extern "C" void fx_adamw_flat(int dtype, float* p, const float* g, float* m, flo
     FX_DISPATCH_T(dtype, adamw_launch<T, true, 256, 2>(FX_ADAMW_ARGS));
   } else {
     FX_DISPATCH_T(dtype, adamw_launch<T, false, 256, 2>(FX_ADAMW_ARGS));
+  }
+#undef FX_ADAMW_ARGS
+}
+
+// the same with a 16-bit gradient (model dtype)
+extern "C" void fx_adamw_flat_g16(int dtype, float* p, const void* g, float* m, float* v,
+                                  void* p16, long n, float lr, float beta1, float beta2, float eps,
+                                  float wd, float l2, const float* gscale, const int* skip,
+                                  const int* step, hipStream_t st) {
+#define FX_ADAMW_ARGS p, g, m, v, p16, n, lr, beta1, beta2, eps, wd, l2, gscale, skip, step, st
+  if (g_adamw_wide) {
+    FX_DISPATCH_T(dtype, (adamw_launch<T, true, 1024, 4, true>(FX_ADAMW_ARGS)));
+  } else if (g_adamw_nt) {
+    FX_DISPATCH_T(dtype, (adamw_launch<T, true, 256, 2, true>(FX_ADAMW_ARGS)));
+  } else {
+    FX_DISPATCH_T(dtype, (adamw_launch<T, false, 256, 2, true>(FX_ADAMW_ARGS)));
   }
 #undef FX_ADAMW_ARGS
 }

@@ -206,6 +206,21 @@ class EagerEngine(BasicEngine):
                     prefetch=comm.get("stage3_prefetch", True), stage=self._sharding_stage,
                     reduce_dtype=red)
             else:
+                # 16-bit gradient storage for the GEMM-written weight matrices
+                # (reference O2: GradStorage in the parameter dtype,
+                # tensor_fusion_helper.py:56,72-74): the weight-gradient GEMM
+                # rounds its fp32 tile once and the update reads 2 B instead
+                # of 4 per parameter.  Opt-in ("auto" = fp32): eligible are
+                # bf16 models that write each gradient once per step (no
+                # micro-batch accumulation, no pipeline schedule, no ZeRO)
+                gd = str(comm.get("grad_dtype", "auto"))
+                if gd == "auto":
+                    gd = "float32"
+                gdt = {"float32": torch.float32, "bfloat16": torch.bfloat16,
+                       "float16": torch.float16}[gd]
+                if gdt != torch.float32 and self._accumulate_steps > 1:
+                    raise ValueError("Distributed.comm.grad_dtype=%s needs accumulate_steps == 1 "
+                                     "(gradients are written, not accumulated, in 16 bits)" % gd)
                 # stage 1 (and stage 2 under pipeline parallelism, where the
                 # tied-embedding reduction needs the flat layout)
                 self.buffer = FlatParamGradBuffer(
@@ -216,7 +231,7 @@ class EagerEngine(BasicEngine):
                     embed_group=self.hcg.get_embedding_group() if self.hcg.pp_degree > 1 else None,
                     bucket_mb=comm.get("dp_bucket_mb", 256),
                     overlap=comm.get("overlap_grad_reduce", True),
-                    shard_stage=self._sharding_stage, reduce_dtype=red)
+                    shard_stage=self._sharding_stage, reduce_dtype=red, grad_dtype=gdt)
             if self.lr_scheduler is None and "lr" in configs.Optimizer:
                 self.lr_scheduler = build_lr_scheduler(configs.Optimizer.lr)
             self.optimizer = build_optimizer(configs.Optimizer, self.buffer, self.lr_scheduler,
@@ -254,7 +269,11 @@ class EagerEngine(BasicEngine):
             # and the next step() joins the side stream before rewriting them)
             # (in whole-step graph mode the update is deferred into the next
             # step's captured body: FlatOptimizer.launch_pending)
-            if comm.get("overlap_optimizer", True) and not self._pipeline \
+            # (under pipeline parallelism too: the stage's decoder layers wait
+            # for their own units in their forward pre-hooks, the rest of the
+            # stage -- embedding, final LN, head -- before the schedule starts,
+            # _fit_impl)
+            if comm.get("overlap_optimizer", True) \
                     and hasattr(self.optimizer, "enable_forward_overlap"):
                 self.optimizer.overlap_grid = int(comm.get("overlap_optimizer_grid", 128))
                 self.optimizer.overlap_cus = int(comm.get("overlap_optimizer_cus", 0) or 0)
@@ -436,6 +455,13 @@ class EagerEngine(BasicEngine):
         model = self._module.model
         model.train()
         if self._pipeline:
+            # the stage's parameters outside its decoder layers (embedding,
+            # final LN, LM head) are the update's root unit, launched first:
+            # the schedule never calls the model's own forward, whose
+            # pre-hook waits for it otherwise
+            wait_root = getattr(self.optimizer, "wait_root_update", None)
+            if wait_root is not None:
+                wait_root()
             loss = model.train_batch(self._module.pretreating_batch(batch), self._accumulate_steps)
         else:
             micro = _split_micro(batch, self._accumulate_steps)

@@ -29,7 +29,7 @@ import torch
 from . import _lib
 
 LAY_KC, LAY_MC = 0, 1
-EPI_STORE, EPI_BIAS_GELU, EPI_DGELU, EPI_F32, EPI_BIAS_GELU_ERF, EPI_DGELU_ERF = range(6)
+EPI_STORE, EPI_BIAS_GELU, EPI_DGELU, EPI_F32, EPI_BIAS_GELU_ERF, EPI_DGELU_ERF, EPI_F32B = range(7)
 
 _MODE = os.environ.get("FLEETX_GEMM", "auto")
 
@@ -387,14 +387,20 @@ def covers_wgrad(dy2, x2):
 def linear_wgrad(dy2, x2, out32, accumulate, sq=None):
     """``out32[N,K] (+)= dy2[M,N]^T @ x2[M,K]`` in fp32.  Returns True if done.
 
+    ``out32`` may also be 16-bit (the bf16 gradient storage of
+    ``Distributed.comm.grad_dtype``): fp32 accumulation, one rounding in the
+    epilogue, never ``accumulate``.
+
     ``sq`` (fp32, :func:`sq_slots` long): the epilogue also writes the sums of
-    squares of the values it stores, so the global gradient norm needs no
-    second pass over this weight's gradient (parallel/grad_buffer.py,
-    ``enable_fused_norm``).  Returns False when the kernel cannot (the caller
-    then computes without it)."""
+    squares of the values it stores (of the fp32 values for a 16-bit output),
+    so the global gradient norm needs no second pass over this weight's
+    gradient (parallel/grad_buffer.py, ``enable_fused_norm``).  Returns False
+    when the kernel cannot (the caller then computes without it)."""
     if not enabled() or not _ok(dy2, x2) or dy2.dtype != x2.dtype:
         return False
-    if out32.dtype != torch.float32 or not out32.is_contiguous():
+    out16 = out32.dtype == dy2.dtype
+    if (out32.dtype != torch.float32 and not out16) or not out32.is_contiguous() \
+            or (out16 and accumulate):
         return False
     M, N = dy2.shape
     K = x2.shape[1]
@@ -403,8 +409,8 @@ def linear_wgrad(dy2, x2, out32, accumulate, sq=None):
     # C[N, K] = sum_m A[n, m] B[m, k]: A = dy stored [m][n], B = x stored [m][k]
     if sq is not None and (sq.dtype != torch.float32 or sq.numel() < sq_slots(N, K)):
         raise ValueError("linear_wgrad: sq needs {} fp32 slots".format(sq_slots(N, K)))
-    rc = _launch(_lib.dt_code(dy2.dtype), LAY_MC, LAY_MC, EPI_F32, N, K, M, dy2, dy2.stride(0),
-                 x2, x2.stride(0), out32, K, beta=accumulate, sq=sq,
+    rc = _launch(_lib.dt_code(dy2.dtype), LAY_MC, LAY_MC, EPI_F32B if out16 else EPI_F32, N, K,
+                 M, dy2, dy2.stride(0), x2, x2.stride(0), out32, K, beta=accumulate, sq=sq,
                  ws=_splitk_ws(N, K, M, dy2.device))
     if rc == 0:
         _lib.maybe_sync()

@@ -33,6 +33,8 @@ class ClipGradByNorm(ClipGradByGlobalNorm):
 
 
 def _sumsq(t):
+    if t.dtype != torch.float32:  # 16-bit gradient storage (grad_dtype)
+        return t.float().square().sum()
     if t.is_cuda:
         k = _lib.kernels()
         blocks = k.sumsq_blocks(t.numel())
@@ -93,8 +95,19 @@ class FlatOptimizer:
 
     # ------------------------------------------------------------------ grads
     def grad_views(self):
+        """Gradient of each owned range in its storage dtype (fp32, or the
+        16-bit view of a ``grad_dtype`` category)."""
+        gs = getattr(self.buffer, "grad_slice", None)
+        if gs is not None:
+            return [gs(s, e) for s, e, _ in self.ranges]
         g = self.buffer.grad_flat
         return [g[s:e] for s, e, _ in self.ranges]
+
+    @staticmethod
+    def _adamw_fn(g):
+        """The fused AdamW launcher for a gradient of this storage dtype."""
+        k = _lib.kernels()
+        return k.adamw_flat if g.dtype == torch.float32 else k.adamw_flat_g16
 
     def compute_grad_norm(self):
         """Global L2 norm over the data/model-parallel world (device scalar)."""
@@ -265,6 +278,15 @@ class FlatOptimizer:
                 torch.cuda.current_stream().wait_event(ev)
         return hook
 
+    def wait_root_update(self):
+        """Order the current stream after the overlapped update of the
+        parameters outside every layer unit (pipeline schedules, whose model
+        forward -- the root unit's hook -- never runs)."""
+        if self._overlap_groups is not None:
+            ev = self._unit_events.pop(-1, None)
+            if ev is not None:
+                torch.cuda.current_stream().wait_event(ev)
+
     def _join_overlap(self):
         """Order the current stream after every pending overlapped update."""
         if self._overlap_groups is not None:
@@ -362,12 +384,14 @@ class FusedAdamW(FlatOptimizer):
             # -- on the 1.3B model slicing every view each step kept the GPU
             # waiting ~1.5 ms per step for the next forward
             units = []
+            gviews = self.grad_views()
             for u, pieces in self._overlap_groups:
                 args = []
                 for ri, lo, hi in pieces:
                     s, e, c = self.ranges[ri]
                     a, b = lo - s, hi - s
-                    args.append((self.master[ri][a:b].data_ptr(), gf[lo:hi].data_ptr(),
+                    g = gviews[ri][a:b]
+                    args.append((self._adamw_fn(g), self.master[ri][a:b].data_ptr(), g.data_ptr(),
                                  self.m[ri][a:b].data_ptr(), self.v[ri][a:b].data_ptr(),
                                  pf[lo:hi].data_ptr(), hi - lo,
                                  float(self.weight_decay if c.decay else 0.0)))
@@ -377,14 +401,13 @@ class FusedAdamW(FlatOptimizer):
                                  self.dev_step.data_ptr())
         gs, fi, ds = self._overlap_dev
         lr = float(lr)
-        adamw = k.adamw_flat
         b1, b2, eps = self.beta1, self.beta2, self.eps
         with torch.cuda.stream(os_):
             st = _lib.stream()
             for i, (u, args) in enumerate(self._overlap_args):
                 if grid and i == head:
                     k.adamw_tune(grid, 1, wide)
-                for mp, gp, m1, v1, pp, n, wd in args:
+                for adamw, mp, gp, m1, v1, pp, n, wd in args:
                     adamw(dt, mp, gp, m1, v1, pp, n, lr, b1, b2, eps, wd, 0.0, gs, fi, ds, st)
                 ev = torch.cuda.Event()
                 ev.record(os_)
@@ -425,7 +448,8 @@ class FusedAdamW(FlatOptimizer):
             wd = self.weight_decay if c.decay else 0.0
             st = self._stage[j % 2]
             cur.wait_event(ready)
-            k.adamw_flat(_lib.dt_code(pf.dtype), st[0].data_ptr(), gviews[ri][o:o + n].data_ptr(),
+            self._adamw_fn(gviews[ri])(_lib.dt_code(pf.dtype), st[0].data_ptr(),
+                                       gviews[ri][o:o + n].data_ptr(),
                          st[1].data_ptr(), st[2].data_ptr(), pf[s + o:s + o + n].data_ptr(), n,
                          float(lr), self.beta1, self.beta2, self.eps, float(wd), 0.0,
                          self.gscale.data_ptr(), self.found_inf.data_ptr(),
@@ -454,7 +478,7 @@ class FusedAdamW(FlatOptimizer):
             wd_dec, l2 = (wd, 0.0) if self.decoupled else (0.0, wd)
             out16 = pf[s:e]
             if p.is_cuda:
-                _lib.kernels().adamw_flat(_lib.dt_code(pf.dtype), p.data_ptr(), g.data_ptr(),
+                self._adamw_fn(g)(_lib.dt_code(pf.dtype), p.data_ptr(), g.data_ptr(),
                                           m.data_ptr(), v.data_ptr(), out16.data_ptr(), p.numel(),
                                           float(lr), self.beta1, self.beta2, self.eps,
                                           float(wd_dec), float(l2), self.gscale.data_ptr(),

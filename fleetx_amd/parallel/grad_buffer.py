@@ -47,12 +47,13 @@ def _round_up(n, a):
 
 
 class Category:
-    __slots__ = ("key", "start", "end", "params")
+    __slots__ = ("key", "start", "end", "params", "gview")
 
     def __init__(self, key):
         self.key = key
         self.start = self.end = 0
         self.params = []
+        self.gview = None  # 16-bit gradient storage of a grad16 category
 
     @property
     def decay(self):
@@ -69,6 +70,11 @@ class Category:
     @property
     def norm_excluded(self):
         return self.key[3]
+
+    @property
+    def grad16(self):
+        """Gradient stored in the model's 16-bit dtype (``grad_dtype``)."""
+        return len(self.key) > 4 and self.key[4]
 
 
 class Bucket:
@@ -93,6 +99,15 @@ def _is_gloo(g):
         return False
 
 
+def grad16_eligible(p, fused_wgrad=True):
+    """A weight whose whole gradient is ONE write of the weight-gradient GEMM
+    (fused into main_grad, not a tied weight with a second part): its gradient
+    can be stored in 16 bits straight from the GEMM's fp32 accumulators."""
+    return (p.dim() == 2 and fused_wgrad and bool(getattr(p, "_fx_fused_wgrad_ok", False))
+            and bool(getattr(p, "_fx_gemm_wgrad", False))
+            and getattr(p, "_fx_grad_parts", 1) == 1)
+
+
 def default_decay_fn(name, p):
     """Reference rule: no decay for biases and norm params (``optimizer.py:39-43``)."""
     if p.ndim < 2:
@@ -105,7 +120,8 @@ class FlatParamGradBuffer:
 
     def __init__(self, named_params, dp_group=None, shard_group=None, mp_group=None,
                  embed_group=None, bucket_mb=256, overlap=True, shard_stage=0,
-                 decay_fn=default_decay_fn, reduce_dtype=torch.float32, fused_wgrad=True):
+                 decay_fn=default_decay_fn, reduce_dtype=torch.float32, fused_wgrad=True,
+                 grad_dtype=torch.float32):
         named = [(n, p) for n, p in named_params if p.requires_grad]
         assert named, "no trainable parameters"
         self.dtype = named[0][1].dtype
@@ -117,15 +133,23 @@ class FlatParamGradBuffer:
         self.shard_stage = shard_stage if self.shard_group is not None else 0
         self.overlap = overlap
         self.reduce_dtype = reduce_dtype
+        # 16-bit gradient storage (Distributed.comm.grad_dtype; reference: the
+        # O2 GradStorage in the parameter dtype, tensor_fusion_helper.py:56,72-74)
+        # for the GEMM-written weight matrices; unsharded buffers only, and
+        # only in the model dtype (the GEMM epilogue rounds its fp32 tile once)
+        g16 = grad_dtype in (torch.bfloat16, torch.float16) and grad_dtype == self.dtype \
+            and self.shard_stage == 0
+        self.grad_dtype = grad_dtype if g16 else torch.float32
 
         cats = {}
         for n, p in reversed(named):
             key = (bool(decay_fn(n, p)), bool(getattr(p, "tp_split", False)),
                    bool(getattr(p, "sequence_parallel", False)),
-                   bool(getattr(p, "norm_exclude", False)))
+                   bool(getattr(p, "norm_exclude", False)),
+                   bool(g16 and grad16_eligible(p, fused_wgrad)))
             cats.setdefault(key, Category(key)).params.append((n, p))
         # deterministic category order: big decay/distributed region first
-        order = sorted(cats.keys(), key=lambda k: (not k[0], not k[1], k[2], k[3]))
+        order = sorted(cats.keys(), key=lambda k: (not k[0], not k[1], k[2], k[3], not k[4]))
         self.categories = [cats[k] for k in order]
 
         # shard padding: each category region is a multiple of ALIGN * nshard
@@ -142,6 +166,14 @@ class FlatParamGradBuffer:
         self.numel = off
         self.param_flat = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
         self.grad_flat = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        # a grad16 category's gradients live in the first half of its own
+        # fp32 region, reinterpreted as 16-bit (no extra memory; nothing reads
+        # that region as fp32: every consumer goes through grad_slice)
+        for c in self.categories:
+            if c.grad16:
+                n16 = c.end - c.start
+                c.gview = self.grad_flat[c.start:c.end].view(self.grad_dtype)[:n16]
+        self._cat_bounds = [(c.start, c.end, c) for c in self.categories]
         self.params = []
         for c in self.categories:
             for n, p in c.params:
@@ -149,7 +181,7 @@ class FlatParamGradBuffer:
                 view = self.param_flat[o:o + k].view_as(p)
                 view.copy_(p.data)
                 p.data = view
-                p.main_grad = self.grad_flat[o:o + k].view_as(p)
+                p.main_grad = self.grad_slice(o, o + k).view_as(p)
                 p.grad = None
                 p._fx_fresh = True
                 p._fx_fused_wgrad = bool(getattr(p, "_fx_fused_wgrad_ok", False)) and fused_wgrad
@@ -180,6 +212,23 @@ class FlatParamGradBuffer:
         self._fused_norm = None
         self.early_norm = None
         self._install_hooks()
+
+    # ------------------------------------------------------------------ storage
+    def category_of(self, start):
+        for s, e, c in self._cat_bounds:
+            if s <= start < e:
+                return c
+        raise IndexError(start)
+
+    def grad_slice(self, start, end):
+        """Gradient elements [start, end) of the flat layout (inside one
+        category) in their storage dtype: fp32 ``grad_flat`` or the 16-bit
+        view of a grad16 category."""
+        c = self.category_of(start)
+        if c.gview is None:
+            return self.grad_flat[start:end]
+        assert end <= c.end
+        return c.gview[start - c.start:end - c.start]
 
     # ------------------------------------------------------------------ setup
     def _add_bucket(self, start, end, params):
@@ -273,7 +322,7 @@ class FlatParamGradBuffer:
         with torch.cuda.stream(self._norm_stream):
             self._norm_stream.wait_event(ev)
             i = self._bucket_index[id(b)]
-            self._norm_part[i:i + 1].copy_(_sumsq(self.grad_flat[b.start:b.end]).reshape(1))
+            self._norm_part[i:i + 1].copy_(_sumsq(self.grad_slice(b.start, b.end)).reshape(1))
 
     def _finish_early_norm(self):
         """(distributed_sq, replicated_sq) device scalars, joined to the current stream."""
@@ -336,6 +385,7 @@ class FlatParamGradBuffer:
                 chunks[dist_].append((t_addr + 4 * o, -m if squared else m))
 
         base = self.grad_flat.data_ptr()
+        extra = {True: [], False: []}  # uncovered 16-bit gradients: summed by torch
         for c in self.categories:
             if c.norm_excluded:
                 continue
@@ -348,22 +398,29 @@ class FlatParamGradBuffer:
                     if id(p) in ok:
                         add(p._fx_sq.data_ptr(), p._fx_sq.numel(), c.distributed, squared=True)
             seg = None  # contiguous runs of uncovered parameters (padding is zero)
+
+            def close(seg):
+                if c.gview is not None:
+                    extra[c.distributed].append(self.grad_slice(seg[0], seg[1]))
+                else:
+                    add(base + 4 * seg[0], seg[1] - seg[0], c.distributed)
+
             for n, p in c.params:
                 o, k = self.offsets[id(p)]
                 if id(p) in ok:
                     if seg is not None:
-                        add(base + 4 * seg[0], seg[1] - seg[0], c.distributed)
+                        close(seg)
                         seg = None
                 elif seg is None:
                     seg = [o, o + k]
                 else:
                     seg[1] = o + k
             if seg is not None:
-                add(base + 4 * seg[0], seg[1] - seg[0], c.distributed)
+                close(seg)
         allc = chunks[True] + chunks[False]
         addr = torch.tensor([a for a, _ in allc] or [0], dtype=torch.int64, device=self.device)
         lens = torch.tensor([n for _, n in allc] or [0], dtype=torch.int64, device=self.device)
-        return addr, lens, len(allc), len(chunks[True])
+        return addr, lens, len(allc), len(chunks[True]), extra
 
     def _finish_fused_norm(self):
         from ..ops import _lib
@@ -372,14 +429,19 @@ class FlatParamGradBuffer:
         plan = cache.get(okey)
         if plan is None:
             plan = cache[okey] = self._fused_norm_plan(okey)
-        addr, lens, nch, nd = plan
+        addr, lens, nch, nd, extra = plan
         part = torch.empty(max(nch, 1), dtype=torch.float32, device=self.device)
         if nch:
             _lib.kernels().sumsq_chunks(addr.data_ptr(), lens.data_ptr(), nch, part.data_ptr(),
                                         _lib.stream())
         zero = torch.zeros((), dtype=torch.float32, device=self.device)
-        self.early_norm = (part[:nd].sum() if nd else zero,
-                           part[nd:nch].sum() if nch > nd else zero)
+        dist_sq = part[:nd].sum() if nd else zero
+        rep_sq = part[nd:nch].sum() if nch > nd else zero
+        for t in extra[True]:
+            dist_sq = dist_sq + t.float().square().sum()
+        for t in extra[False]:
+            rep_sq = rep_sq + t.float().square().sum()
+        self.early_norm = (dist_sq, rep_sq)
 
     def _data_groups(self):
         return self.dp_group, self.shard_group
@@ -390,12 +452,15 @@ class FlatParamGradBuffer:
         b.launched = True
         from .linear import join_wgrad_stream
         join_wgrad_stream()  # weight gradients computed on the side stream are final
-        seg = self.grad_flat[b.start:b.end]
+        seg = self.grad_slice(b.start, b.end)
         works = []
         if self._norm_stream is not None:  # _launch only runs on final gradients
             self._early_norm_bucket(b)
-        low = self.reduce_dtype != torch.float32
-        src = seg.to(self.reduce_dtype) if low else seg   # 16-bit wire copy
+        # wire copy in the reduce dtype only for fp32 storage reduced in 16 bits and only
+        # when a collective runs; 16-bit gradient storage is reduced in place
+        low = (self.reduce_dtype != seg.dtype and seg.dtype == torch.float32
+               and (self.dp_group is not None or self.shard_group is not None))
+        src = seg.to(self.reduce_dtype) if low else seg
         if self.shard_stage >= 1 and self.shard_group is not None:
             # reduce-scatter to the owner (in place: RCCL's recvbuff = sendbuff + rank*count);
             # dp all-reduce of the owned shard follows in finish()
@@ -452,7 +517,7 @@ class FlatParamGradBuffer:
         if self.mp_group is not None:
             for c in self.categories:
                 if c.seq_parallel:
-                    dist.all_reduce(self.grad_flat[c.start:c.end], group=self.mp_group.group)
+                    dist.all_reduce(self.grad_slice(c.start, c.end), group=self.mp_group.group)
         # tied embedding between first and last pipeline stage
         if self.embed_group is not None:
             for n, p in self.params:

@@ -210,18 +210,25 @@ def _accumulate_wgrad(weight, dy2, x2, bias=None, notify=True, bias_notify=True,
         else:
             db = db.to(bias.dtype)
     a, b = tn if tn is not None else (dy2.t(), x2)
-    if dy2.dtype == torch.float32:
+    if mg.dtype != torch.float32:
+        # 16-bit gradient storage (grad_dtype): the vendor GEMM's own fp32
+        # accumulation, rounded once into main_grad
+        if fresh:
+            torch.mm(a, b, out=mg)
+        else:
+            mg.add_(torch.mm(a, b))
+    elif dy2.dtype == torch.float32:
         if fresh:
             torch.mm(a, b, out=mg)
         else:
             mg.addmm_(a, b)
-    elif _mm_out_supported():
+    elif _mm_out_supported() and dy2.is_cuda:
         if fresh:
             torch.ops.aten.mm.dtype_out(a, b, torch.float32, out=mg)
         else:
             torch.ops.aten.addmm.dtype_out(mg, a, b, torch.float32, out=mg)
-    else:  # pragma: no cover - older torch
-        g = torch.mm(a, b)
+    else:  # CPU 16-bit models / older torch: fp32 product
+        g = torch.mm(a.float(), b.float())
         if fresh:
             mg.copy_(g)
         else:

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 5: GEMM plan generation, full GPU suite, 6.7B step A/B of bf16 gradient storage
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r5h
+mkdir -p $O
+timeout -k 10 900 python3 -u tools/gemm_plan.py --out $O/gemm_plan_gfx950.json > $O/plan.jsonl 2> $O/plan.err || { tail -5 $O/plan.err; exit 1; }
+tail -1 $O/plan.err
+timeout -k 10 1500 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?
+tail -3 $O/pytest_gpu.log
+[ $rc -ne 0 ] && exit $rc
+for i in 1 2; do
+timeout -k 10 400 python3 -u bench.py --steps 10 --warmup 5 > $O/bench_g16_$i.log 2>&1 || { tail -5 $O/bench_g16_$i.log; exit 1; }
+echo g16; grep -o '"ms_per_step": [0-9.]*\|"final_loss": [0-9a-zA-Z.]*\|"peak_mem_gb": [0-9.]*' $O/bench_g16_$i.log
+FLEETX_BENCH_OVERRIDES="Distributed.comm.grad_dtype=float32" timeout -k 10 400 python3 -u bench.py --steps 10 --warmup 5 > $O/bench_g32_$i.log 2>&1 || { tail -5 $O/bench_g32_$i.log; exit 1; }
+echo g32; grep -o '"ms_per_step": [0-9.]*\|"final_loss": [0-9a-zA-Z.]*\|"peak_mem_gb": [0-9.]*' $O/bench_g32_$i.log
+done

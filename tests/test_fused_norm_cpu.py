@@ -41,12 +41,14 @@ def _buffer():
     return buf
 
 
-def _emulate(addr, lens, nch, nd):
+def _emulate(addr, lens, nch, nd, extra=None):
     part = []
     for a, n in zip(addr.tolist()[:nch], lens.tolist()[:nch]):
         vals = (ctypes.c_float * abs(n)).from_address(a)
         part.append(sum(float(x) for x in vals) if n < 0 else sum(float(x) ** 2 for x in vals))
-    return sum(part[:nd]), sum(part[nd:])
+    ex = extra or {True: [], False: []}   # uncovered 16-bit gradients (summed by torch)
+    return (sum(part[:nd]) + sum(float(t.double().pow(2).sum()) for t in ex[True]),
+            sum(part[nd:]) + sum(float(t.double().pow(2).sum()) for t in ex[False]))
 
 
 @pytest.mark.parametrize("covered", ["all", "some", "none"])

@@ -403,3 +403,25 @@ def test_persistent_under_memory_pressure(gemm, persist_mode, act):
         torch.cuda.current_stream().wait_stream(s)
         assert torch.equal(y, ref)
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("M,N,K", [(1024, 768, 512), (8192, 1024, 1024), (16448, 1408, 1408),
+                                   (256, 4096, 4096)])
+def test_wgrad_16bit_out(gemm, M, N, K):
+    """EPI_F32B: the weight gradient written in bf16 from the fp32
+    accumulators (16-bit gradient storage), split-K shapes included; the norm
+    partials are the sums of squares of the fp32 values."""
+    torch.manual_seed(10)
+    dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    ref = dy.float().t() @ x.float()
+    out = torch.full((N, K), float("nan"), device="cuda", dtype=torch.bfloat16)
+    sq = torch.zeros(gemm.sq_slots(N, K), device="cuda")
+    assert gemm.linear_wgrad(dy, x, out, False, sq=sq)
+    assert _rel(out, ref) < 1e-2
+    # one rounding of the fp32 result: as close to it as bf16 allows
+    assert torch.equal(out, ref.to(torch.bfloat16)) or \
+        float((out.float() - ref).abs().max()) <= float(ref.abs().max()) * 2 ** -7
+    assert abs(float(sq.double().sum()) - float(ref.double().pow(2).sum())) < \
+        1e-4 * float(ref.double().pow(2).sum())
+    assert not gemm.linear_wgrad(dy, x, out, True)  # 16-bit gradients are never accumulated

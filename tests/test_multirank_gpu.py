@@ -80,7 +80,8 @@ def _train_gpu(rank, world, layout, steps=3, extra=()):
     from fleetx_amd.ops import _lib
     return {"losses": losses, "gnorms": gnorms, "pnorm": _master_norm(eng), "drank": drank,
             "native": _lib.kernels() is not None, "master": gather_master_state(eng),
-            "master0": master0}
+            "master0": master0,
+            "overlap": getattr(eng.optimizer, "_overlap_groups", None) is not None}
 
 
 def _master_norm(eng):
@@ -148,14 +149,16 @@ def _check(results, ref_run):
             (r["pnorm"], ref_run["pnorm"])
     # ... and tensor by tensor in the single-rank layout, against the tensor's
     # own bf16-noise scale (ref_gpu["noise"]: the single-rank run with another
-    # micro-batch split): err <= 3 x noise + 2 % of the tensor's update (+ a
-    # 1e-4 relative floor).  A permuted or misplaced shard gives ~140 % of the
-    # update; a 20 % gradient-scale error confined to one shard moves that
-    # shard's update by ~20 % -- both far outside the noise.
+    # micro-batch split) plus 10 % of the tensor's update: TP layouts add the
+    # rounding of bf16 activation all-reduces, ~6 % of the update on the
+    # row-parallel FC2 weight (profiles/r5_multirank/).  A permuted or
+    # misplaced shard gives ~140 % of the update; a 20 % gradient-scale error
+    # confined to one of two shards ~14 % -- both outside the bound (round 4
+    # allowed 30 %).
     check_master_against_noise(results[0]["master"], ref_run)
 
 
-def check_master_against_noise(got, ref_run, k=3.0, rel=0.02):
+def check_master_against_noise(got, ref_run, k=3.0, rel=0.10):
     ref, ref0, noise = ref_run["master"], ref_run["master0"], ref_run["noise"]
     names = set(x.replace("#tied", "") for x in got)
     assert names == set(ref), sorted(names ^ set(ref))
@@ -237,3 +240,25 @@ def test_fused_lm_head_ce_matches_single_rank(ref_gpu, name):
     out = dist_utils.run(_train_gpu_fused_head, 1 if name == "single" else 2, layout,
                          timeout=300)
     _check(out, ref_gpu)
+
+
+def _train_gpu_det(rank, world, layout, overlap):
+    os.environ["FLEETX_DETERMINISTIC"] = "1"
+    return _train_gpu(rank, world, layout,
+                      extra=("Distributed.comm.overlap_optimizer=%s" % overlap,))
+
+
+@pytest.mark.parametrize("name", ["pp2_1f1b", "pp2_interleaved"])
+def test_pipeline_overlapped_update_is_bitwise_serial(name):
+    """Under pipeline parallelism the update of step N runs on the side
+    stream beside step N+1's schedule (each stage's layers wait for their own
+    units, the embedding / final LN / head for the root unit before the
+    schedule starts): bitwise the serial update."""
+    a = dist_utils.run(_train_gpu_det, 2, LAYOUTS[name], True, timeout=300)
+    b = dist_utils.run(_train_gpu_det, 2, LAYOUTS[name], False, timeout=300)
+    assert all(r["overlap"] for r in a) and not any(r["overlap"] for r in b)
+    for ra, rb in zip(a, b):
+        assert ra["losses"] == rb["losses"], (ra["losses"], rb["losses"])
+        assert set(ra["master"]) == set(rb["master"])
+        for k in ra["master"]:
+            assert torch.equal(ra["master"][k], rb["master"][k]), k
