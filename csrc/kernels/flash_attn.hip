@@ -301,6 +301,7 @@ struct AttnParams {
   float drop_scale;
   int dval;              // valid head dim (<= the tile's D; columns past it are zero)
   const uint64_t* salt;  // graph mode: per-replay device salt (fx_set_dropout_salt)
+  int pair;              // causal forward: two query blocks per workgroup (fa_fwd_kernel)
 };
 
 // per-(batch, head) dropout hash seed; under graph mode the baked key is
@@ -482,6 +483,15 @@ __device__ __forceinline__ void fwd_tile(const AttnParams& P, const Frag<D>& F, 
 // ============================================================================
 // forward: WG = 4 waves x 32 queries = 128 queries; KV tile = 64 keys
 // ============================================================================
+// Causal grids pair query blocks: workgroup p of a head runs block nq-1-p
+// (the heaviest) and then block p (the lightest) through ONE K/V tile stream,
+// so every workgroup carries the same nq+1 blocks' worth of tiles, the grid is
+// half as many workgroups, and the second block's Q fragments and first K/V
+// tile load under the first block's last tile instead of in a fresh
+// workgroup's exposed prologue.  (fa_pair_grid(): FLEETX_FA_PAIR=0 restores
+// one block per workgroup in LPT order.)
+__device__ __forceinline__ bool fa_pair_on(const AttnParams& P) { return P.pair != 0; }
+
 template <typename T, int D, bool CAUSAL, bool DROP, bool KB, int NW>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -490,16 +500,26 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
   Frag<D> F;
   F.init(lane);
   const int nq = (P.Sq + QB - 1) / QB;
-  const int nblk = nq * P.B * P.H;
-  const int lid = xcd_remap(blockIdx.x, nblk);
-  int bh, qblock;
-  if constexpr (CAUSAL) {
-    int rank;
-    lpt_order(lid, nq, P.B * P.H, bh, rank);
-    qblock = nq - 1 - rank;
+  // work items of this workgroup: query block qa, then (paired causal) qb2 >= 0
+  int bh, qa, qb2 = -1;
+  if (CAUSAL && fa_pair_on(P)) {
+    const int npair = (nq + 1) >> 1;
+    const int lid = xcd_remap(blockIdx.x, npair * P.B * P.H);
+    bh = lid / npair;
+    const int p = lid - bh * npair;
+    qa = nq - 1 - p;
+    qb2 = p != qa ? p : -1;
   } else {
-    bh = lid / nq;
-    qblock = lid % nq;
+    const int nblk = nq * P.B * P.H;
+    const int lid = xcd_remap(blockIdx.x, nblk);
+    if constexpr (CAUSAL) {
+      int rank;
+      lpt_order(lid, nq, P.B * P.H, bh, rank);
+      qa = nq - 1 - rank;
+    } else {
+      bh = lid / nq;
+      qa = lid % nq;
+    }
   }
   const int b = bh / P.H, hd = bh % P.H;
 
@@ -509,20 +529,27 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
   int kv_len = P.Sk;
   if (P.kv_lens) kv_len = min(kv_len, P.kv_lens[b]);
 
-  const int wq0 = qblock * QB + w * 32;
-  const int qi = wq0 + (lane & 31);
-  short8 qf[D / 16];
+  auto load_q = [&](int qblock, short8 (&qf)[D / 16]) {
+    const int qi_ = qblock * QB + w * 32 + (lane & 31);
 #pragma unroll
-  for (int s = 0; s < D / 16; ++s) {
-    if (qi < P.Sq && 16 * s + 8 * h < P.dval)
-      qf[s] = *reinterpret_cast<const short8*>(qp + (long)qi * P.sq_s + 16 * s + 8 * h);
-    else
-      qf[s] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
-  }
+    for (int s = 0; s < D / 16; ++s) {
+      if (qi_ < P.Sq && 16 * s + 8 * h < P.dval)
+        qf[s] = *reinterpret_cast<const short8*>(qp + (long)qi_ * P.sq_s + 16 * s + 8 * h);
+      else
+        qf[s] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  };
+  auto tiles_of = [&](int qblock) {
+    const int e = CAUSAL ? min(kv_len, (qblock + 1) * QB) : kv_len;
+    return (e + KV - 1) / KV;
+  };
 
-  int kv_end = kv_len;
-  if (CAUSAL) kv_end = min(kv_end, (qblock + 1) * QB);
-  const int ntiles = (kv_end + KV - 1) / KV;
+  int wq0 = qa * QB + w * 32;
+  int qi = wq0 + (lane & 31);
+  short8 qf[D / 16];
+  load_q(qa, qf);
+  const int ntA = tiles_of(qa);
+  const int ntiles = ntA + (qb2 >= 0 ? tiles_of(qb2) : 0);
 
   floatx16 oacc[D / 32];
 #pragma unroll
@@ -533,9 +560,35 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
   const float sl2 = P.scale * LOG2E;
   const uint32_t cb = DROP ? attn_cb(P, bh) : 0u;
 
+  // O and lse of the current item (its rows are qi of the current wq0)
+  auto finish = [&]() {
+    const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+    const float inv = ltot > 0.f ? (DROP ? P.drop_scale : 1.f) / ltot : 0.f;
+    if (qi < P.Sq) {
+      uint16_t* op = P.out + b * P.so_b + hd * P.so_h + (long)qi * P.so_s;
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          ushort4 o;
+          o.x = Elt<T>::from_f(oacc[dt][4 * g + 0] * inv);
+          o.y = Elt<T>::from_f(oacc[dt][4 * g + 1] * inv);
+          o.z = Elt<T>::from_f(oacc[dt][4 * g + 2] * inv);
+          o.w = Elt<T>::from_f(oacc[dt][4 * g + 3] * inv);
+          if (dt * 32 + 8 * g + 4 * h < P.dval)
+            *reinterpret_cast<ushort4*>(op + dt * 32 + 8 * g + 4 * h) = o;
+        }
+      if (h == 0)
+        P.lse[(long)bh * P.Sq + qi] = ltot > 0.f ? (m_run + log2f(ltot)) * LN2 : INFINITY;
+    }
+  };
+
+  // the tile stream covers both items (tile t >= ntA is tile t - ntA of the
+  // second); rows are clamped at kv_len only -- causal masking is per element
   GldsStream<D, KV, NW> kld, vld;
-  kld.init(kp, P.sk_s, kv_end, w, lane, P.dval);
-  vld.init(vp, P.sv_s, kv_end, w, lane, P.dval);
+  kld.init(kp, P.sk_s, kv_len, w, lane, P.dval);
+  vld.init(vp, P.sv_s, kv_len, w, lane, P.dval);
+  auto row_of = [&](int t) { return (t < ntA ? t : t - ntA) * KV; };
   if (ntiles > 0) {
     kld.load(0, smem, lane);
     vld.load(0, smem + 2 * TB, lane);
@@ -543,40 +596,42 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
   glds_wait();
   __syncthreads();
 
+  short8 qn[D / 16];  // the second item's Q fragments, loaded under the first's last tile
   for (int it = 0; it < ntiles; ++it) {
     const int cur = it & 1;
     const char* kt = smem + cur * TB;
     const char* vt = smem + 2 * TB + cur * TB;
     const bool more = it + 1 < ntiles;
+    const bool switch_item = qb2 >= 0 && it == ntA - 1;
+    if (switch_item) load_q(qb2, qn);
     if (more) {
-      kld.load((it + 1) * KV, smem + (cur ^ 1) * TB, lane);
-      vld.load((it + 1) * KV, smem + 2 * TB + (cur ^ 1) * TB, lane);
+      kld.load(row_of(it + 1), smem + (cur ^ 1) * TB, lane);
+      vld.load(row_of(it + 1), smem + 2 * TB + (cur ^ 1) * TB, lane);
     }
-    const int kb = it * KV;
-    fwd_tile<T, D, CAUSAL, DROP, KB>(P, F, kt, vt, qf, oacc, m_run, lsum, kb, wq0, qi, kv_len, b,
-                                     h, sl2, cb);
+    fwd_tile<T, D, CAUSAL, DROP, KB>(P, F, kt, vt, qf, oacc, m_run, lsum, row_of(it), wq0, qi,
+                                     kv_len, b, h, sl2, cb);
+    if (switch_item) {
+      finish();
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) oacc[dt][i] = 0.f;
+      m_run = -INFINITY;
+      lsum = 0.f;
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) qf[s] = qn[s];
+      wq0 = qb2 * QB + w * 32;
+      qi = wq0 + (lane & 31);
+    }
     glds_wait();
     __syncthreads();
   }
-
-  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
-  const float inv = ltot > 0.f ? (DROP ? P.drop_scale : 1.f) / ltot : 0.f;
-  if (qi < P.Sq) {
-    uint16_t* op = P.out + b * P.so_b + hd * P.so_h + (long)qi * P.so_s;
-#pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        ushort4 o;
-        o.x = Elt<T>::from_f(oacc[dt][4 * g + 0] * inv);
-        o.y = Elt<T>::from_f(oacc[dt][4 * g + 1] * inv);
-        o.z = Elt<T>::from_f(oacc[dt][4 * g + 2] * inv);
-        o.w = Elt<T>::from_f(oacc[dt][4 * g + 3] * inv);
-        if (dt * 32 + 8 * g + 4 * h < P.dval)
-          *reinterpret_cast<ushort4*>(op + dt * 32 + 8 * g + 4 * h) = o;
-      }
-    if (h == 0) P.lse[(long)bh * P.Sq + qi] = ltot > 0.f ? (m_run + log2f(ltot)) * LN2 : INFINITY;
+  if (qb2 >= 0 && ntA == 0) {  // kv_len == 0: no tile switched the items; both rows are empty
+    finish();
+    wq0 = qb2 * QB + w * 32;
+    qi = wq0 + (lane & 31);
   }
+  finish();
 }
 
 // ============================================================================
@@ -1078,6 +1133,15 @@ static int waves_for(int n) {
   return idle3 < idle4 ? 3 : 4;
 }
 
+// FLEETX_FA_PAIR=0: one causal query block per workgroup (LPT order) instead of pairs
+static bool fa_pair_grid() {
+  static const bool on = [] {
+    const char* e = getenv("FLEETX_FA_PAIR");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 static int fwd_waves() {
   static int nw = [] {
     const char* e = getenv("FLEETX_FA_FWD_WAVES");
@@ -1147,7 +1211,8 @@ static int flash_fwd_t(const void* q, const void* k, const void* v, void* out, f
   P.so_b = os[0]; P.so_s = os[1]; P.so_h = os[2];
   const int nw = D == 96 ? waves_for(Sq) : fwd_waves();
   const int nq = (Sq + 32 * nw - 1) / (32 * nw);
-  const int grid = nq * B * H;
+  P.pair = causal && fa_pair_grid() ? 1 : 0;
+  const int grid = (P.pair ? (nq + 1) / 2 : nq) * B * H;
   const size_t smem = 4 * 64 * D * 2;
   const bool drop = p > 0.f, kb = kbias != nullptr;
   if (nw == 8) {

@@ -192,15 +192,30 @@ __device__ __forceinline__ void st_stream(V x, V* a, bool nt) {
 // G16: the gradient is stored in the model's 16-bit dtype (the bf16
 // gradient storage of Distributed.comm.grad_dtype: 2 B read per parameter
 // instead of 4 -- 28 instead of 30 B per parameter per step)
+// The raw gradient group (4 x 16 bit or 4 x fp32) is loaded with the other
+// streams and widened only in the compute loop: widening it at the load made
+// the compiler wait for each group's gradient before issuing the next group's
+// loads (4 loads in flight per lane instead of 4U; gfx950 ISA of the G16
+// instance), and the G16 update ran 14 % longer than the fp32 one beside the
+// forward GEMMs (profiles/r5_grad16/).
+template <bool G16>
+struct GradRaw { using type = floatx4; };
+template <>
+struct GradRaw<true> { using type = unsigned long long; };
+
+template <bool G16>
+__device__ __forceinline__ typename GradRaw<G16>::type adamw_ld_grad(const void* g, long i,
+                                                                      bool nt) {
+  return ld_stream(reinterpret_cast<const typename GradRaw<G16>::type*>(g) + i, nt);
+}
+
 template <typename T, bool G16>
-__device__ __forceinline__ floatx4 adamw_ld_grad(const void* g, long i, bool nt) {
-  if constexpr (G16) {
-    const unsigned long long h = ld_stream(reinterpret_cast<const unsigned long long*>(g) + i, nt);
+__device__ __forceinline__ floatx4 adamw_widen(typename GradRaw<G16>::type h) {
+  if constexpr (G16)
     return floatx4{Elt<T>::to_f((uint16_t)h), Elt<T>::to_f((uint16_t)(h >> 16)),
                    Elt<T>::to_f((uint16_t)(h >> 32)), Elt<T>::to_f((uint16_t)(h >> 48))};
-  } else {
-    return ld_stream(reinterpret_cast<const floatx4*>(g) + i, nt);
-  }
+  else
+    return h;
 }
 
 template <typename T, bool G16>
@@ -227,13 +242,14 @@ __global__ __launch_bounds__(BS) void adamw_flat_kernel(
   const long n4 = n / 4;
   const long stride = (long)gridDim.x * (BS * U);
   for (long i0 = blockIdx.x * (long)(BS * U) + threadIdx.x; i0 < n4; i0 += stride) {
-    floatx4 pp[U], gg[U], mm[U], vv[U];
+    floatx4 pp[U], mm[U], vv[U];
+    typename GradRaw<G16>::type gg[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long i = i0 + (long)u * BS;
       if (i < n4) {
         pp[u] = ld_stream(reinterpret_cast<const floatx4*>(p) + i, NT);
-        gg[u] = adamw_ld_grad<T, G16>(g, i, NT);
+        gg[u] = adamw_ld_grad<G16>(g, i, NT);
         mm[u] = ld_stream(reinterpret_cast<const floatx4*>(m) + i, NT);
         vv[u] = ld_stream(reinterpret_cast<const floatx4*>(v) + i, NT);
       }
@@ -243,7 +259,7 @@ __global__ __launch_bounds__(BS) void adamw_flat_kernel(
       const long i = i0 + (long)u * BS;
       if (i >= n4) break;
       floatx4 pa = pp[u], ma = mm[u], va = vv[u];
-      const floatx4 ga = gg[u];
+      const floatx4 ga = adamw_widen<T, G16>(gg[u]);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float gr = ga[j] * gs + l2 * pa[j];

@@ -210,12 +210,15 @@ class EagerEngine(BasicEngine):
                 # (reference O2: GradStorage in the parameter dtype,
                 # tensor_fusion_helper.py:56,72-74): the weight-gradient GEMM
                 # rounds its fp32 tile once and the update reads 2 B instead
-                # of 4 per parameter.  Opt-in ("auto" = fp32): eligible are
-                # bf16 models that write each gradient once per step (no
-                # micro-batch accumulation, no pipeline schedule, no ZeRO)
+                # of 4 per parameter.  "auto": bf16 models that write each
+                # gradient once per step (no micro-batch accumulation, no
+                # pipeline schedule, no ZeRO); fp32 otherwise.  6.7B step on
+                # one MI355X: -4.4 ms (profiles/r5_grad16/)
                 gd = str(comm.get("grad_dtype", "auto"))
                 if gd == "auto":
-                    gd = "float32"
+                    gd = "bfloat16" if (self._dtype == torch.bfloat16
+                                        and self._accumulate_steps == 1 and not self._pipeline
+                                        and self._sharding_stage == 0) else "float32"
                 gdt = {"float32": torch.float32, "bfloat16": torch.bfloat16,
                        "float16": torch.float16}[gd]
                 if gdt != torch.float32 and self._accumulate_steps > 1:
