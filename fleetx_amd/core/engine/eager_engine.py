@@ -276,6 +276,11 @@ class EagerEngine(BasicEngine):
             # for their own units in their forward pre-hooks, the rest of the
             # stage -- embedding, final LN, head -- before the schedule starts,
             # _fit_impl)
+            # ZeRO-1/2: the post-update parameter all-gather hides under the next forward
+            # (and, with overlap_optimizer, the owned shard's update before it)
+            if comm.get("overlap_param_gather", True) and not self._pipeline \
+                    and hasattr(self.buffer, "enable_param_gather_overlap"):
+                self.buffer.enable_param_gather_overlap(model)
             if comm.get("overlap_optimizer", True) \
                     and hasattr(self.optimizer, "enable_forward_overlap"):
                 self.optimizer.overlap_grid = int(comm.get("overlap_optimizer_grid", 128))
@@ -301,10 +306,6 @@ class EagerEngine(BasicEngine):
             elif comm.get("fused_grad_norm", True) and hasattr(self.buffer, "enable_fused_norm") \
                     and getattr(self.optimizer, "grad_clip", None) is not None:
                 self.buffer.enable_fused_norm()
-            # ZeRO-1/2: the post-update parameter all-gather hides under the next forward
-            if comm.get("overlap_param_gather", True) and not self._pipeline \
-                    and hasattr(self.buffer, "enable_param_gather_overlap"):
-                self.buffer.enable_param_gather_overlap(model)
             if self._pipeline:
                 model.attach(self)
             if self.device.type == "cuda":

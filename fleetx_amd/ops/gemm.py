@@ -350,15 +350,19 @@ def linear_fwd(x2, w, bias=None, act=None, out=None):
     return y if act is None else (y, h)
 
 
-def linear_dgrad(dy2, w, act_input=None, act="gelu"):
-    """``dy2 [M,N] @ w [N,K]`` (times ``gelu'(act_input)`` when given)."""
+def linear_dgrad(dy2, w, act_input=None, act="gelu", out=None):
+    """``dy2 [M,N] @ w [N,K]`` (times ``gelu'(act_input)`` when given), into
+    ``out`` (a contiguous [M, K] block) when given."""
     if not enabled() or not _ok(dy2, w, act_input) or w.dtype != dy2.dtype:
         return None
     M, N = dy2.shape
     K = w.shape[1]
     if w.shape[0] != N:
         raise ValueError("linear_dgrad: shape mismatch")
-    dx = torch.empty(M, K, device=dy2.device, dtype=dy2.dtype)
+    if out is not None and (out.shape != (M, K) or not out.is_contiguous()
+                            or out.dtype != dy2.dtype or out.data_ptr() % 16):
+        return None
+    dx = out if out is not None else torch.empty(M, K, device=dy2.device, dtype=dy2.dtype)
     epi = EPI_STORE
     ld_aux = 0
     if act_input is not None:

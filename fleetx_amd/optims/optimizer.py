@@ -188,7 +188,8 @@ class FlatOptimizer:
             self._pending = self.get_lr()  # launched by the next step (launch_pending)
         else:
             self._update(self.get_lr())
-        self.buffer.allgather_params()
+        if not self._overlap_gather:  # (else the overlapped update gathers bucket by bucket)
+            self.buffer.allgather_params()
 
     # Whole-step graph mode (Engine.cuda_graph): the forward-overlapped update
     # of step N is launched at the START of step N+1's captured body, so one
@@ -232,9 +233,10 @@ class FlatOptimizer:
         returns False (and changes nothing) otherwise."""
         from ..parallel.sharding import find_layer_units
         buf = self.buffer
-        if (buf.device.type != "cuda" or self.offload or getattr(buf, "shard_stage", 0) != 0
-                or not hasattr(buf, "offsets")):
+        if buf.device.type != "cuda" or self.offload or not hasattr(buf, "offsets"):
             return False
+        if getattr(buf, "shard_stage", 0) != 0:
+            return self._enable_sharded_overlap()
         units = find_layer_units(model)
         if not units:
             return False
@@ -269,6 +271,36 @@ class FlatOptimizer:
         self._overlap_hooks = [model.register_forward_pre_hook(self._make_wait(-1))]
         for i, m in enumerate(units):
             self._overlap_hooks.append(m.register_forward_pre_hook(self._make_wait(i)))
+        return True
+
+    _overlap_gather = False
+
+    def _enable_sharded_overlap(self):
+        """ZeRO-1 (and stage 2 under pipeline parallelism, which keeps the
+        flat buffer): the owned shard of each gradient bucket is updated on the
+        side stream in the order the next forward first uses the buckets, and
+        the bucket's parameter all-gather is issued on that stream right after
+        its update -- so the update AND the gather hide under the next forward,
+        whose layers already wait only for the gathers of their own buckets
+        (``FlatParamGradBuffer.enable_param_gather_overlap``; reference: the
+        stage-1 optimizer step then ``broadcast``/gather of
+        ``dygraph_sharding_optimizer``, serial after backward).  Needs the
+        overlapped parameter gather (not under pipeline schedules)."""
+        buf = self.buffer
+        if getattr(buf, "shard_stage", 0) not in (1, 2) or getattr(buf, "_ag_need", None) is None:
+            return False
+        bucket_of = {}
+        for ri, (s, e, c) in enumerate(self.ranges):
+            bi = next(i for i, b in enumerate(buf.buckets) if b.start <= s < b.end)
+            bucket_of.setdefault(bi, []).append((ri, s, e))
+        # every bucket is gathered, also those where this rank owns nothing
+        self._overlap_groups = [(bi, [p for p in bucket_of.get(bi, []) if p[2] > p[1]])
+                                for bi in buf._ag_order]
+        self._overlap_gather = True
+        from ..utils.streams import side_stream
+        self._opt_stream = side_stream(buf.device)
+        self._unit_events = {}
+        self._overlap_hooks = []
         return True
 
     def _make_wait(self, unit):
@@ -319,6 +351,8 @@ class FlatOptimizer:
         if flushed:
             self.launch_pending()
         self._join_overlap()
+        if self._overlap_gather:  # ZeRO: the gathers the overlapped update issued
+            self.buffer.sync_params()
         if flushed:
             # a captured step launches this update again at its start: with
             # the skip flag set it leaves the applied update alone (the step's
@@ -409,6 +443,9 @@ class FusedAdamW(FlatOptimizer):
                     k.adamw_tune(grid, 1, wide)
                 for adamw, mp, gp, m1, v1, pp, n, wd in args:
                     adamw(dt, mp, gp, m1, v1, pp, n, lr, b1, b2, eps, wd, 0.0, gs, fi, ds, st)
+                if self._overlap_gather:  # ZeRO: this bucket's gather follows its update
+                    self.buffer.gather_bucket_async(u)
+                    continue
                 ev = torch.cuda.Event()
                 ev.record(os_)
                 self._unit_events[u] = ev

@@ -595,17 +595,22 @@ class FlatParamGradBuffer:
                 w.wait()
             self._ag_works = {}
 
-    def _allgather_async(self):
+    def gather_bucket_async(self, bi):
+        """Issue bucket ``bi``'s parameter all-gather on the current stream
+        (ordered after whatever that stream ran before, e.g. the bucket's
+        update); the forward pre-hooks of the layers using it wait for it."""
         n, r = self.shard_group.nranks, self.shard_group.rank
+        b = self.buckets[bi]
+        chunk = (b.end - b.start) // n
+        full = self.param_flat[b.start:b.end]
+        mine = full[r * chunk:(r + 1) * chunk].clone()
+        w = dist.all_gather_into_tensor(full, mine, group=self.shard_group.group, async_op=True)
+        self._ag_works[bi] = (w, mine)  # keep the send buffer alive until waited
+
+    def _allgather_async(self):
         self.sync_params()
         for bi in self._ag_order:
-            b = self.buckets[bi]
-            chunk = (b.end - b.start) // n
-            full = self.param_flat[b.start:b.end]
-            mine = full[r * chunk:(r + 1) * chunk].clone()
-            w = dist.all_gather_into_tensor(full, mine, group=self.shard_group.group,
-                                            async_op=True)
-            self._ag_works[bi] = (w, mine)  # keep the send buffer alive until waited
+            self.gather_bucket_async(bi)
 
     def allgather_params(self):
         """After a sharded update, every rank gathers the full model-dtype params."""

@@ -56,7 +56,10 @@ def _mm_into(a2, w, out2, bias=None):
 
 
 def _dgrad_into(dy2, w, out2):
-    """``out2 = dy2 @ w``."""
+    """``out2 = dy2 @ w`` (the MFMA kernel when the shipped plan / route
+    picks it for this shape, as the non-SP data gradients)."""
+    if G.use("dgrad", dy2, w) and G.linear_dgrad(dy2, w, out=out2) is not None:
+        return
     torch.mm(dy2, w, out=out2)
 
 

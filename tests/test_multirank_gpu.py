@@ -248,12 +248,17 @@ def _train_gpu_det(rank, world, layout, overlap):
                       extra=("Distributed.comm.overlap_optimizer=%s" % overlap,))
 
 
-@pytest.mark.parametrize("name", ["pp2_1f1b", "pp2_interleaved"])
-def test_pipeline_overlapped_update_is_bitwise_serial(name):
-    """Under pipeline parallelism the update of step N runs on the side
-    stream beside step N+1's schedule (each stage's layers wait for their own
-    units, the embedding / final LN / head for the root unit before the
-    schedule starts): bitwise the serial update."""
+@pytest.mark.parametrize("name", ["pp2_1f1b", "pp2_interleaved", "zero1"])
+def test_overlapped_update_is_bitwise_serial(name):
+    """Multi-rank layouts keep the forward-overlapped update: under pipeline
+    parallelism the update of step N runs on the side stream beside step
+    N+1's schedule (each stage's layers wait for their own units, the
+    embedding / final LN / head for the root unit before the schedule
+    starts); under ZeRO-1 each bucket's owned shard is updated on the side
+    stream and its parameter all-gather issued right behind it, and the
+    layers wait for their buckets' gathers (ZeRO-2/3 keep their own
+    sharded buffer, ``parallel/sharding.py``, with a serial update).
+    Bitwise the serial update."""
     a = dist_utils.run(_train_gpu_det, 2, LAYOUTS[name], True, timeout=300)
     b = dist_utils.run(_train_gpu_det, 2, LAYOUTS[name], False, timeout=300)
     assert all(r["overlap"] for r in a) and not any(r["overlap"] for r in b)
