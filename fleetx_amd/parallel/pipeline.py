@@ -41,10 +41,42 @@ import torch.distributed as dist
 from . import collective_check
 
 
+class _GlooStaged:
+    """A gloo p2p op on a DEVICE tensor, staged through host memory.  gloo
+    moves the bytes from its own thread with no order against the GPU
+    stream: a send could read an activation its producing kernel has not
+    finished writing (the multi-rank rehearsal of ``bench.py`` over gloo saw
+    NaN losses come and go with kernel timing).  The send copies to the host
+    first (after the producer, on the current stream); the receive lands in a
+    host buffer and is copied to the device tensor when waited."""
+
+    __slots__ = ("work", "host", "dev")
+
+    def __init__(self, work, host=None, dev=None):
+        self.work, self.host, self.dev = work, host, dev
+
+    def wait(self):
+        self.work.wait()
+        if self.dev is not None:
+            self.dev.copy_(self.host, non_blocking=False)
+            self.dev = None
+        return True
+
+
 def issue_dist(group, ops):
     """Issue ``ops`` (``[(kind, tensor, peer)]``, kind ``"send"``/``"recv"``,
     peer a global rank) as one grouped call; returns the ``Work`` list (one
     per op on gloo, one for the whole group on RCCL)."""
+    if ops and ops[0][1].is_cuda and dist.get_backend(group) == "gloo":
+        works = []
+        for k, t, peer in ops:
+            if k == "send":
+                host = t.to("cpu")  # (synchronous: after the kernels that produce t)
+                works.append(_GlooStaged(dist.isend(host, peer, group=group), host))
+            else:
+                host = torch.empty(t.shape, dtype=t.dtype)
+                works.append(_GlooStaged(dist.irecv(host, peer, group=group), host, t))
+        return works
     return dist.batch_isend_irecv([dist.P2POp(dist.isend if k == "send" else dist.irecv,
                                               t, peer, group) for k, t, peer in ops])
 
