@@ -47,6 +47,13 @@ void fx_adamw_flat(int, float*, const float*, float*, float*, void*, long, float
 void fx_adamw_flat_g16(int, float*, const void*, float*, float*, void*, long, float, float,
                        float, float, float, float, const float*, const int*, const int*,
                        hipStream_t);
+int fx_adamw_flat_pk(int, void*, const void*, float*, float*, void*, long, float, float, float,
+                     float, float, float, const float*, const int*, const int*, hipStream_t);
+int fx_adamw_flat_pk_g16(int, void*, const void*, float*, float*, void*, long, float, float,
+                         float, float, float, float, const float*, const int*, const int*,
+                         hipStream_t);
+void fx_pk_split(const float*, void*, void*, long, hipStream_t);
+void fx_pk_join(const void*, const void*, float*, long, hipStream_t);
 void fx_cast_f32(int, const float*, void*, long, hipStream_t);
 void fx_accum_f32(int, float*, const void*, long, int, hipStream_t);
 void fx_embedding_fwd(int, const int64_t*, const int64_t*, const void*, const void*, void*, int,
@@ -223,6 +230,27 @@ PYBIND11_MODULE(_kernels, m) {
     fx_adamw_flat_g16(dt, F(p), CP(g), F(mm), F(vv), P(p16), n, lr, b1, b2, eps, wd, l2,
                       F(gscale), reinterpret_cast<const int*>(skip),
                       reinterpret_cast<const int*>(step), S(st));
+  });
+  // packed master: p = the master's low halves, p16 = the bf16 parameters (high halves)
+  m.def("adamw_flat_pk", [](int dt, ptr p, ptr g, ptr mm, ptr vv, ptr p16, long n, float lr,
+                            float b1, float b2, float eps, float wd, float l2, ptr gscale,
+                            ptr skip, ptr step, ptr st) {
+    return fx_adamw_flat_pk(dt, P(p), CP(g), F(mm), F(vv), P(p16), n, lr, b1, b2, eps, wd, l2,
+                            F(gscale), reinterpret_cast<const int*>(skip),
+                            reinterpret_cast<const int*>(step), S(st));
+  });
+  m.def("adamw_flat_pk_g16", [](int dt, ptr p, ptr g, ptr mm, ptr vv, ptr p16, long n, float lr,
+                                float b1, float b2, float eps, float wd, float l2, ptr gscale,
+                                ptr skip, ptr step, ptr st) {
+    return fx_adamw_flat_pk_g16(dt, P(p), CP(g), F(mm), F(vv), P(p16), n, lr, b1, b2, eps, wd,
+                                l2, F(gscale), reinterpret_cast<const int*>(skip),
+                                reinterpret_cast<const int*>(step), S(st));
+  });
+  m.def("pk_split", [](ptr x, ptr hi, ptr lo, long n, ptr st) {
+    fx_pk_split(F(x), P(hi), P(lo), n, S(st));
+  });
+  m.def("pk_join", [](ptr hi, ptr lo, ptr x, long n, ptr st) {
+    fx_pk_join(CP(hi), CP(lo), F(x), n, S(st));
   });
   m.def("cast_f32", [](int dt, ptr x, ptr y, long n, ptr st) {
     fx_cast_f32(dt, F(x), P(y), n, S(st));

@@ -224,7 +224,41 @@ __device__ __forceinline__ float adamw_grad1(const void* g, long i) {
   else return reinterpret_cast<const float*>(g)[i];
 }
 
-template <typename T, bool NT, int BS, int U, bool G16 = false>
+// Packed master (PK, bf16 models): the fp32 master x is stored as the bf16
+// parameter itself (hi) plus x's low 16 bits (lo), so the update reads and
+// writes 2 + 2 B of master+parameter instead of 4 + 4 (fp32 master) + 2
+// (parameter copy): 26 instead of 28 B per parameter with bf16 gradients.
+// hi = x's high half rounded to nearest on the low half (ties toward zero);
+// x = ((hi - (lo > 0x8000)) << 16) | lo is exact, so the master keeps every
+// fp32 bit and the parameter differs from a round-to-nearest-even cast only
+// when the low half is exactly 0x8000.
+__device__ __forceinline__ float pk_decode(uint32_t hi, uint32_t lo) {
+  const uint32_t top = hi - (lo > 0x8000u ? 1u : 0u);
+  return __uint_as_float((top << 16) | lo);
+}
+__device__ __forceinline__ void pk_encode(float x, uint32_t& hi, uint32_t& lo) {
+  const uint32_t b = __float_as_uint(x);
+  lo = b & 0xffffu;
+  hi = ((b >> 16) + (lo > 0x8000u ? 1u : 0u)) & 0xffffu;
+}
+
+// One element of the update with every rounding spelled out (explicit fma,
+// no contraction left to the compiler): each kernel instance -- fp32 / 16-bit
+// gradient, packed / fp32 master, vector body / scalar tail -- computes the
+// same bits, whatever the vectorizer makes of the surrounding code.
+__device__ __forceinline__ void adamw_elem(float& p, float& m, float& v, float g, float gs,
+                                           float l2, float beta1, float beta2,
+                                           float inv_sqrt_bc2, float eps, float decay,
+                                           float step_size) {
+#pragma clang fp contract(off)
+  const float gr = __builtin_fmaf(g, gs, l2 * p);
+  m = __builtin_fmaf(beta1, m, (1.f - beta1) * gr);
+  v = __builtin_fmaf(beta2, v, ((1.f - beta2) * gr) * gr);
+  const float denom = __builtin_fmaf(__builtin_sqrtf(v), inv_sqrt_bc2, eps);
+  p = __builtin_fmaf(p, decay, -((step_size * m) / denom));
+}
+
+template <typename T, bool NT, int BS, int U, bool G16 = false, bool PK = false>
 __global__ __launch_bounds__(BS) void adamw_flat_kernel(
     float* __restrict__ p, const void* __restrict__ g, float* __restrict__ m,
     float* __restrict__ v, uint16_t* __restrict__ p16, long n, float lr, float beta1,
@@ -243,12 +277,18 @@ __global__ __launch_bounds__(BS) void adamw_flat_kernel(
   const long stride = (long)gridDim.x * (BS * U);
   for (long i0 = blockIdx.x * (long)(BS * U) + threadIdx.x; i0 < n4; i0 += stride) {
     floatx4 pp[U], mm[U], vv[U];
+    unsigned long long ph[PK ? U : 1], pl[PK ? U : 1];  // PK: raw hi / lo halves
     typename GradRaw<G16>::type gg[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long i = i0 + (long)u * BS;
       if (i < n4) {
-        pp[u] = ld_stream(reinterpret_cast<const floatx4*>(p) + i, NT);
+        if constexpr (PK) {
+          ph[u] = ld_stream(reinterpret_cast<const unsigned long long*>(p16) + i, NT);
+          pl[u] = ld_stream(reinterpret_cast<const unsigned long long*>(p) + i, NT);
+        } else {
+          pp[u] = ld_stream(reinterpret_cast<const floatx4*>(p) + i, NT);
+        }
         gg[u] = adamw_ld_grad<G16>(g, i, NT);
         mm[u] = ld_stream(reinterpret_cast<const floatx4*>(m) + i, NT);
         vv[u] = ld_stream(reinterpret_cast<const floatx4*>(v) + i, NT);
@@ -258,19 +298,40 @@ __global__ __launch_bounds__(BS) void adamw_flat_kernel(
     for (int u = 0; u < U; ++u) {
       const long i = i0 + (long)u * BS;
       if (i >= n4) break;
-      floatx4 pa = pp[u], ma = mm[u], va = vv[u];
+      floatx4 pa, ma = mm[u], va = vv[u];
+      if constexpr (PK) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          pa[j] = pk_decode((uint32_t)(ph[u] >> (16 * j)) & 0xffffu,
+                            (uint32_t)(pl[u] >> (16 * j)) & 0xffffu);
+      } else {
+        pa = pp[u];
+      }
       const floatx4 ga = adamw_widen<T, G16>(gg[u]);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float gr = ga[j] * gs + l2 * pa[j];
-        ma[j] = beta1 * ma[j] + (1.f - beta1) * gr;
-        va[j] = beta2 * va[j] + (1.f - beta2) * gr * gr;
-        const float denom = sqrtf(va[j]) * inv_sqrt_bc2 + eps;
-        pa[j] = pa[j] * decay - step_size * ma[j] / denom;
+        float pj = pa[j], mj = ma[j], vj = va[j];
+        adamw_elem(pj, mj, vj, ga[j], gs, l2, beta1, beta2, inv_sqrt_bc2, eps, decay, step_size);
+        pa[j] = pj;
+        ma[j] = mj;
+        va[j] = vj;
       }
-      st_stream(pa, reinterpret_cast<floatx4*>(p) + i, NT);
       st_stream(ma, reinterpret_cast<floatx4*>(m) + i, NT);
       st_stream(va, reinterpret_cast<floatx4*>(v) + i, NT);
+      if constexpr (PK) {
+        unsigned long long hw = 0, lw = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint32_t hj, lj;
+          pk_encode(pa[j], hj, lj);
+          hw |= (unsigned long long)hj << (16 * j);
+          lw |= (unsigned long long)lj << (16 * j);
+        }
+        st_stream(hw, reinterpret_cast<unsigned long long*>(p16) + i, NT);
+        st_stream(lw, reinterpret_cast<unsigned long long*>(p) + i, NT);
+        continue;
+      }
+      st_stream(pa, reinterpret_cast<floatx4*>(p) + i, NT);
       if (p16) {
         ushort4 o;
         o.x = Elt<T>::from_f(pa[0]);
@@ -282,13 +343,41 @@ __global__ __launch_bounds__(BS) void adamw_flat_kernel(
     }
   }
   for (long i = n4 * 4 + blockIdx.x * (long)BS + threadIdx.x; i < n; i += (long)gridDim.x * BS) {
-    const float gr = adamw_grad1<T, G16>(g, i) * gs + l2 * p[i];
-    m[i] = beta1 * m[i] + (1.f - beta1) * gr;
-    v[i] = beta2 * v[i] + (1.f - beta2) * gr * gr;
-    const float denom = sqrtf(v[i]) * inv_sqrt_bc2 + eps;
-    p[i] = p[i] * decay - step_size * m[i] / denom;
-    if (p16) p16[i] = Elt<T>::from_f(p[i]);
+    uint16_t* plo = reinterpret_cast<uint16_t*>(p);
+    float x = PK ? pk_decode(p16[i], plo[i]) : p[i];
+    float mi = m[i], vi = v[i];
+    adamw_elem(x, mi, vi, adamw_grad1<T, G16>(g, i), gs, l2, beta1, beta2, inv_sqrt_bc2, eps,
+               decay, step_size);
+    m[i] = mi;
+    v[i] = vi;
+    if constexpr (PK) {
+      uint32_t hj, lj;
+      pk_encode(x, hj, lj);
+      p16[i] = (uint16_t)hj;
+      plo[i] = (uint16_t)lj;
+    } else {
+      p[i] = x;
+      if (p16) p16[i] = Elt<T>::from_f(x);
+    }
   }
+}
+
+// packed-master helpers for checkpoints / tests: fp32 master <-> (hi, lo)
+__global__ __launch_bounds__(256) void pk_split_kernel(const float* __restrict__ x,
+                                                       uint16_t* __restrict__ hi,
+                                                       uint16_t* __restrict__ lo, long n) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    uint32_t h, l;
+    pk_encode(x[i], h, l);
+    hi[i] = (uint16_t)h;
+    lo[i] = (uint16_t)l;
+  }
+}
+__global__ __launch_bounds__(256) void pk_join_kernel(const uint16_t* __restrict__ hi,
+                                                      const uint16_t* __restrict__ lo,
+                                                      float* __restrict__ x, long n) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    x[i] = pk_decode(hi[i], lo[i]);
 }
 
 template <typename T>
@@ -448,7 +537,7 @@ extern "C" void fx_adamw_tune(int grid, int nt, int wide) {
   g_adamw_wide = wide;
 }
 
-template <typename T, bool NT, int BS, int U, bool G16 = false>
+template <typename T, bool NT, int BS, int U, bool G16 = false, bool PK = false>
 static void adamw_launch(float* p, const void* g, float* m, float* v, void* p16, long n,
                          float lr, float beta1, float beta2, float eps, float wd, float l2,
                          const float* gscale, const int* skip, const int* step, hipStream_t st) {
@@ -458,7 +547,7 @@ static void adamw_launch(float* p, const void* g, float* m, float* v, void* p16,
   const long cap = 256L * (8 * 256 / BS) * 4;
   int grid = (int)(blocks < 1 ? 1 : (blocks > cap ? cap : blocks));
   if (g_adamw_grid > 0 && g_adamw_grid < grid) grid = g_adamw_grid;
-  adamw_flat_kernel<T, NT, BS, U, G16><<<grid, BS, 0, st>>>(p, g, m, v, (uint16_t*)p16, n, lr, beta1,
+  adamw_flat_kernel<T, NT, BS, U, G16, PK><<<grid, BS, 0, st>>>(p, g, m, v, (uint16_t*)p16, n, lr, beta1,
                                                       beta2, eps, wd, l2, gscale, skip, step,
                                                       g_adamw_lr);
 }
@@ -492,6 +581,49 @@ extern "C" void fx_adamw_flat_g16(int dtype, float* p, const void* g, float* m, 
     FX_DISPATCH_T(dtype, (adamw_launch<T, false, 256, 2, true>(FX_ADAMW_ARGS)));
   }
 #undef FX_ADAMW_ARGS
+}
+
+// packed master (bf16 models only): `p` is the master's low-half array, `p16`
+// the bf16 parameters (= the high halves), read and written
+#define FX_ADAMW_PK(G16)                                                                     \
+  do {                                                                                       \
+    if (dtype != 0) return -1;                                                               \
+    if (g_adamw_wide)                                                                        \
+      adamw_launch<bf16, true, 1024, 4, G16, true>(FX_ADAMW_ARGS);                           \
+    else if (g_adamw_nt)                                                                     \
+      adamw_launch<bf16, true, 256, 2, G16, true>(FX_ADAMW_ARGS);                            \
+    else                                                                                     \
+      adamw_launch<bf16, false, 256, 2, G16, true>(FX_ADAMW_ARGS);                           \
+    return 0;                                                                                \
+  } while (0)
+extern "C" int fx_adamw_flat_pk(int dtype, void* lo, const void* g, float* m, float* v, void* hi,
+                                long n, float lr, float beta1, float beta2, float eps, float wd,
+                                float l2, const float* gscale, const int* skip, const int* step,
+                                hipStream_t st) {
+  float* p = (float*)lo;
+  void* p16 = hi;
+#define FX_ADAMW_ARGS p, g, m, v, p16, n, lr, beta1, beta2, eps, wd, l2, gscale, skip, step, st
+  FX_ADAMW_PK(false);
+#undef FX_ADAMW_ARGS
+}
+extern "C" int fx_adamw_flat_pk_g16(int dtype, void* lo, const void* g, float* m, float* v,
+                                    void* hi, long n, float lr, float beta1, float beta2,
+                                    float eps, float wd, float l2, const float* gscale,
+                                    const int* skip, const int* step, hipStream_t st) {
+  float* p = (float*)lo;
+  void* p16 = hi;
+#define FX_ADAMW_ARGS p, g, m, v, p16, n, lr, beta1, beta2, eps, wd, l2, gscale, skip, step, st
+  FX_ADAMW_PK(true);
+#undef FX_ADAMW_ARGS
+}
+#undef FX_ADAMW_PK
+
+// fp32 master <-> (bf16 parameter, low halves)
+extern "C" void fx_pk_split(const float* x, void* hi, void* lo, long n, hipStream_t st) {
+  pk_split_kernel<<<grid_n(n), 256, 0, st>>>(x, (uint16_t*)hi, (uint16_t*)lo, n);
+}
+extern "C" void fx_pk_join(const void* hi, const void* lo, float* x, long n, hipStream_t st) {
+  pk_join_kernel<<<grid_n(n), 256, 0, st>>>((const uint16_t*)hi, (const uint16_t*)lo, x, n);
 }
 
 extern "C" void fx_cast_f32(int dtype, const float* x, void* y, long n, hipStream_t st) {

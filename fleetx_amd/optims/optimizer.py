@@ -85,6 +85,62 @@ class FlatOptimizer:
         self.last_grad_norm = torch.zeros((), dtype=torch.float32, device=dev)
         self.loss_scale = None  # set by the engine for fp16 (device tensor)
 
+    # ------------------------------------------------------------------ master
+    # Packed master (Optimizer.packed_master; bf16 models, device-resident
+    # state): the fp32 master of each range is the bf16 parameter itself (its
+    # high half, rounded on the low half) plus a 16-bit array of low halves,
+    # joined exactly inside the AdamW kernel (loss_optim_embed.hip pk_decode).
+    # The update moves 26 instead of 28 B per parameter (bf16 gradients) and
+    # the master takes 2 instead of 4 B of HBM.  ``master`` decodes fp32
+    # copies for checkpoints, tests and state gathers.
+    _lo = None
+    _master = None
+
+    @property
+    def master(self):
+        if self._lo is None:
+            return self._master
+        return [self._join(ri) for ri in range(len(self.ranges))]
+
+    @master.setter
+    def master(self, value):
+        self._master = value
+
+    def _maybe_pack_master(self, want):
+        pf = getattr(self.buffer, "param_flat", None)
+        if not want or self.offload or pf is None or pf.device.type != "cuda" \
+                or pf.dtype != torch.bfloat16 or self._master is None:
+            return False
+        self._lo = [torch.zeros(e - s, dtype=torch.int16, device=pf.device)
+                    for s, e, _ in self.ranges]
+        for (s, e, _), lo, m in zip(self.ranges, self._lo, self._master):
+            _lib.kernels().pk_split(m.data_ptr(), pf[s:e].data_ptr(), lo.data_ptr(), e - s,
+                                    _lib.stream())
+        self._master = None  # the fp32 copies are gone: hi = the parameters, lo above
+        return True
+
+    def _join(self, ri):
+        s, e, _ = self.ranges[ri]
+        x = torch.empty(e - s, dtype=torch.float32, device=self._lo[ri].device)
+        _lib.kernels().pk_join(self.buffer.param_flat[s:e].data_ptr(), self._lo[ri].data_ptr(),
+                               x.data_ptr(), e - s, _lib.stream())
+        return x
+
+    def _mslice(self, ri, a, b):
+        """The master storage of range ``ri`` [a, b) the kernel addresses:
+        fp32 values, or (packed) the 16-bit low halves."""
+        return (self._lo if self._lo is not None else self._master)[ri][a:b]
+
+    def _set_master(self, ri, src):
+        """Overwrite range ``ri``'s master (and, packed, its parameters) with fp32 ``src``."""
+        if self._lo is None:
+            self._master[ri].copy_(src)
+            return
+        s, e, _ = self.ranges[ri]
+        x = src.to(device=self._lo[ri].device, dtype=torch.float32).contiguous()
+        _lib.kernels().pk_split(x.data_ptr(), self.buffer.param_flat[s:e].data_ptr(),
+                                self._lo[ri].data_ptr(), e - s, _lib.stream())
+
     # ------------------------------------------------------------------ lr
     def get_lr(self):
         return self._lr() if callable(self._lr) else float(self._lr)
@@ -103,10 +159,12 @@ class FlatOptimizer:
         g = self.buffer.grad_flat
         return [g[s:e] for s, e, _ in self.ranges]
 
-    @staticmethod
-    def _adamw_fn(g):
-        """The fused AdamW launcher for a gradient of this storage dtype."""
+    def _adamw_fn(self, g):
+        """The fused AdamW launcher for a gradient of this storage dtype (and
+        the packed master layout)."""
         k = _lib.kernels()
+        if self._lo is not None:
+            return k.adamw_flat_pk if g.dtype == torch.float32 else k.adamw_flat_pk_g16
         return k.adamw_flat if g.dtype == torch.float32 else k.adamw_flat_g16
 
     def compute_grad_norm(self):
@@ -341,6 +399,10 @@ class FlatOptimizer:
 
     def refresh_master_from_params(self):
         self.sync_state()
+        if self._lo is not None:  # master = the parameters exactly: low halves 0
+            for lo in self._lo:
+                lo.zero_()
+            return
         for (s, e, _), m in zip(self.ranges, self.master):
             m.copy_(self.buffer.param_flat[s:e].float())
 
@@ -377,6 +439,7 @@ class FusedAdamW(FlatOptimizer):
                          kw.get("check_group"), kw.get("pp_group"), kw.get("mp_group"),
                          offload=kw.get("offload", False))
         self.beta1, self.beta2, self.eps = float(beta1), float(beta2), float(epsilon)
+        self._maybe_pack_master(kw.get("packed_master", False))
         if self.offload:
             self.m = [torch.zeros(x.numel(), dtype=torch.float32, pin_memory=True)
                       for x in self.master]
@@ -389,8 +452,9 @@ class FusedAdamW(FlatOptimizer):
                            for _ in range(2)]
             self._copy_stream = torch.cuda.Stream(device=dev)
         else:
-            self.m = [torch.zeros_like(x) for x in self.master]
-            self.v = [torch.zeros_like(x) for x in self.master]
+            dev = buffer.device
+            self.m = [torch.zeros(e - s, dtype=torch.float32, device=dev) for s, e, _ in self.ranges]
+            self.v = [torch.zeros(e - s, dtype=torch.float32, device=dev) for s, e, _ in self.ranges]
 
     def _update_overlapped(self, lr):
         """AdamW per unit (root first, then layer 0, 1, ...) on the side
@@ -425,7 +489,7 @@ class FusedAdamW(FlatOptimizer):
                     s, e, c = self.ranges[ri]
                     a, b = lo - s, hi - s
                     g = gviews[ri][a:b]
-                    args.append((self._adamw_fn(g), self.master[ri][a:b].data_ptr(), g.data_ptr(),
+                    args.append((self._adamw_fn(g), self._mslice(ri, a, b).data_ptr(), g.data_ptr(),
                                  self.m[ri][a:b].data_ptr(), self.v[ri][a:b].data_ptr(),
                                  pf[lo:hi].data_ptr(), hi - lo,
                                  float(self.weight_decay if c.decay else 0.0)))
@@ -507,7 +571,8 @@ class FusedAdamW(FlatOptimizer):
         if self._overlap_groups is not None and self.decoupled:
             return self._update_overlapped(lr)
         pf = self.buffer.param_flat
-        for (s, e, c), g, p, m, v in zip(self.ranges, self.grad_views(), self.master, self.m,
+        masters = [self._mslice(ri, 0, e - s) for ri, (s, e, _) in enumerate(self.ranges)]
+        for (s, e, c), g, p, m, v in zip(self.ranges, self.grad_views(), masters, self.m,
                                          self.v):
             wd = self.weight_decay if c.decay else 0.0
             # AdamW: decoupled decay on the weights; Adam: L2 term added to the
@@ -516,7 +581,7 @@ class FusedAdamW(FlatOptimizer):
             out16 = pf[s:e]
             if p.is_cuda:
                 self._adamw_fn(g)(_lib.dt_code(pf.dtype), p.data_ptr(), g.data_ptr(),
-                                          m.data_ptr(), v.data_ptr(), out16.data_ptr(), p.numel(),
+                                          m.data_ptr(), v.data_ptr(), out16.data_ptr(), e - s,
                                           float(lr), self.beta1, self.beta2, self.eps,
                                           float(wd_dec), float(l2), self.gscale.data_ptr(),
                                           self.found_inf.data_ptr(), self.dev_step.data_ptr(),
@@ -546,17 +611,18 @@ class FusedAdamW(FlatOptimizer):
         self.sync_state()
         self.step_count = state["step"]
         self.dev_step.fill_(int(state.get("applied_step", state["step"])))
-        for dst, src in zip(self.master, state["master"]):
-            dst.copy_(src)
+        for ri, src in enumerate(state["master"]):
+            self._set_master(ri, src)
         for dst, src in zip(self.m, state["m"]):
             dst.copy_(src)
         for dst, src in zip(self.v, state["v"]):
             dst.copy_(src)
         if hasattr(self._lr, "set_state_dict") and isinstance(state.get("lr"), dict):
             self._lr.set_state_dict(state["lr"])
-        pf = self.buffer.param_flat
-        for (s, e, _), p in zip(self.ranges, self.master):
-            pf[s:e].copy_(p)
+        if self._lo is None:  # (packed: _set_master wrote the parameters)
+            pf = self.buffer.param_flat
+            for (s, e, _), p in zip(self.ranges, self.master):
+                pf[s:e].copy_(p)
 
 
 class AdamW(FusedAdamW):
