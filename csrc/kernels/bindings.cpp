@@ -97,6 +97,7 @@ int fx_gemm_tuned(long*, int);
 void fx_gemm_set_tuned(int, int, int, int, int, int, int);
 void fx_gemm_set_tune(int);
 void fx_gemm_set_persist(int);
+void fx_gemm_set_xrect(int);
 int fx_decode_gemv(int, int, int, int, int, const void*, long, const void*, long, const void*,
                    const void*, long, void*, long, void*, void*, const long*, int, int, int,
                    const void*, const void*, float, hipStream_t);
@@ -355,6 +356,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("gemm_set_tuned", &fx_gemm_set_tuned);
   m.def("gemm_set_tune", &fx_gemm_set_tune);
   m.def("gemm_set_persist", &fx_gemm_set_persist);
+  m.def("gemm_set_xrect", &fx_gemm_set_xrect);
   m.def("gemm_tuned", []() {
     std::vector<long> buf(7 * 512);
     const int n = fx_gemm_tuned(buf.data(), (int)buf.size());

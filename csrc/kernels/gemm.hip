@@ -32,6 +32,7 @@ int fx_gemm5_launch(int dt, int la, int lb, int epi, const fxg::GemmParams& P, h
 long fx_gemm5_ws_bytes(int M, int N, int K);
 void fx_gemm5_set_geom(int nf, int split);
 void fx_gemm5_set_persist(int on);
+void fx_gemm5_set_xrect(int on);
 
 using namespace fxg;
 
@@ -50,7 +51,11 @@ static int g_gm = -1;  // FLEETX_GEMM_GM / fx_gemm_set_gm: force the tile-order 
 // every gm.
 static int g_tune = -1;
 static std::map<std::tuple<int, int, int, int, int, int>, int> g_gm_tuned;
-static const int kGmCand[] = {1, 2, 4, 8, 16};
+// order codes: the M-group height, + 32 = within XCD rectangles (gemm5.hip
+// g5_tile_mn: each XCD's range of tile ids is one rectangle of the grid, so
+// its L2 holds that rectangle's panels; 6.7B forward L2 misses -23 %,
+// profiles/r5_xrect/)
+static const int kGmCand[] = {1, 2, 4, 8, 16, 33, 34, 36, 40, 48};
 
 static int gemm_tuned_gm(int dt, int la, int lb, int epi, const GemmParams& P0, hipStream_t st) {
   const int f32 = epi_wgrad(epi);
@@ -161,6 +166,10 @@ extern "C" void fx_gemm_set_geom(int nf, int split) { fx_gemm5_set_geom(nf, spli
 // Persistent 16-bit launches on (1) / off (0, one workgroup per tile) for
 // A/B runs and the bitwise test; < 0 = FLEETX_GEMM5_PERSIST.
 extern "C" void fx_gemm_set_persist(int on) { fx_gemm5_set_persist(on); }
+
+// XCD-rectangle tile mapping forced on (1) / off (2), 0 = per order code;
+// < 0 = FLEETX_GEMM_XRECT
+extern "C" void fx_gemm_set_xrect(int on) { fx_gemm5_set_xrect(on); }
 
 // The tuned table: (la, lb, fp32 out, M, N, K, gm) rows, flattened.
 extern "C" int fx_gemm_tuned(long* out, int cap) {

@@ -51,6 +51,11 @@ struct GemmParams {
   // EPI_F32B: 1 = this launch stores the 16-bit gradient, 0 = fp32 split-K
   // partial slabs (the combine stores the 16-bit result)
   int out16;
+  // XCD rectangles (gemm5): > 0 = the tile grid is cut into xm x (8 / xm)
+  // equal rectangles, rectangle r = tile ids [r * T / 8, (r + 1) * T / 8) = the
+  // range xcd_remap / the persistent queues deal to XCD r; the gm order runs
+  // inside each rectangle.  0 = the gm order over the whole grid.
+  int xm;
 };
 
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {

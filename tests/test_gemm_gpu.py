@@ -425,3 +425,44 @@ def test_wgrad_16bit_out(gemm, M, N, K):
     assert abs(float(sq.double().sum()) - float(ref.double().pow(2).sum())) < \
         1e-4 * float(ref.double().pow(2).sum())
     assert not gemm.linear_wgrad(dy, x, out, True)  # 16-bit gradients are never accumulated
+
+
+# XCD rectangles (gemm5 ``P.xm``, FLEETX_GEMM_XRECT): each XCD's range of tile
+# ids is one rectangle of the tile grid.  A permutation of which workgroup
+# computes which tile: bitwise the plain order for every kind (persistent and
+# one-per-tile forwards, data gradients, split-K fp32 and 16-bit weight
+# gradients).  Shapes whose 256- / 128-tile grids cut into 8 equal rectangles.
+@pytest.fixture
+def xrect_mode(gemm):
+    from fleetx_amd.ops import _lib
+    yield _lib.kernels().gemm_set_xrect
+    _lib.kernels().gemm_set_xrect(-1)
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 6144, 512), (2048, 2048, 1024), (8192, 1024, 1024)])
+def test_xcd_rectangles_are_bitwise_the_plain_order(gemm, persist_mode, xrect_mode, M, N, K):
+    torch.manual_seed(11)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    outs = {}
+    for xr in (2, 1):  # forced off / on
+        xrect_mode(xr)
+        res = []
+        for pm in (0, 1):
+            persist_mode(pm)
+            res.append(gemm.linear_fwd(x, w, b))
+        res.append(gemm.linear_fwd(x, w, b, act="gelu")[0])
+        res.append(gemm.linear_dgrad(dy, w))
+        dw = torch.empty(N, K, device="cuda", dtype=torch.float32)
+        assert gemm.linear_wgrad(dy, x, dw, False)
+        res.append(dw)
+        dw16 = torch.empty(N, K, device="cuda", dtype=torch.bfloat16)
+        assert gemm.linear_wgrad(dy, x, dw16, False)
+        res.append(dw16)
+        outs[xr] = res
+    for a, c in zip(outs[2], outs[1]):
+        assert torch.equal(a, c)
+    assert _rel(outs[1][0], x.float() @ w.float().t() + b.float()) < 1e-2
+    assert _rel(outs[1][4], dy.float().t() @ x.float()) < 1e-3
