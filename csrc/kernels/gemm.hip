@@ -51,11 +51,12 @@ static int g_gm = -1;  // FLEETX_GEMM_GM / fx_gemm_set_gm: force the tile-order 
 // every gm.
 static int g_tune = -1;
 static std::map<std::tuple<int, int, int, int, int, int>, int> g_gm_tuned;
-// order codes: the M-group height, + 32 = within XCD rectangles (gemm5.hip
+// order codes: the M-group height, + 32 = within XCD rectangles, + 64 = the
+// runner-up rectangle cut (gemm5.hip
 // g5_tile_mn: each XCD's range of tile ids is one rectangle of the grid, so
 // its L2 holds that rectangle's panels; 6.7B forward L2 misses -23 %,
 // profiles/r5_xrect/)
-static const int kGmCand[] = {1, 2, 4, 8, 16, 33, 34, 36, 40, 48};
+static const int kGmCand[] = {1, 2, 4, 8, 16, 33, 34, 36, 40, 48, 97, 98, 100, 104};
 
 static int gemm_tuned_gm(int dt, int la, int lb, int epi, const GemmParams& P0, hipStream_t st) {
   const int f32 = epi_wgrad(epi);

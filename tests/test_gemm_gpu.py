@@ -466,3 +466,27 @@ def test_xcd_rectangles_are_bitwise_the_plain_order(gemm, persist_mode, xrect_mo
         assert torch.equal(a, c)
     assert _rel(outs[1][0], x.float() @ w.float().t() + b.float()) < 1e-2
     assert _rel(outs[1][4], dy.float().t() @ x.float()) < 1e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 16384, 512), (2048, 8192, 1024)])
+def test_tile_order_codes_are_bitwise_equal(gemm, M, N, K):
+    """Every tile-order code (M-group height, XCD rectangles, the runner-up
+    rectangle cut) computes each tile with the same arithmetic."""
+    from fleetx_amd.ops import _lib
+    k = _lib.kernels()
+    torch.manual_seed(12)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    outs = []
+    try:
+        for code in (1, 4, 33, 36, 97, 100):
+            k.gemm_set_gm(code)
+            dw = torch.empty(N, K, device="cuda", dtype=torch.float32)
+            assert gemm.linear_wgrad(dy, x, dw, False)
+            outs.append((gemm.linear_fwd(x, w), gemm.linear_dgrad(dy, w), dw))
+    finally:
+        k.gemm_set_gm(0)
+    for o in outs[1:]:
+        for a, c in zip(outs[0], o):
+            assert torch.equal(a, c)

@@ -43,9 +43,9 @@ MODELS = {
     "vitg": (16448, [("qkv", 1408, 4224), ("out", 1408, 1408), ("fc1", 1408, 6144),
                      ("fc2", 6144, 1408)]),
 }
-# tile-order codes: M-group height, + 32 = inside XCD rectangles (csrc/kernels/gemm5.hip
-# g5_tile_mn)
-GMS = (1, 2, 4, 8, 16, 33, 34, 36, 40, 48)
+# tile-order codes: M-group height, + 32 = inside XCD rectangles, + 64 = the runner-up
+# rectangle cut (csrc/kernels/gemm5.hip g5_tile_mn / g5_xrect_rows)
+GMS = (1, 2, 4, 8, 16, 33, 34, 36, 40, 48, 97, 98, 100, 104)
 
 
 def med_time(fns, rounds, iters):
