@@ -472,6 +472,8 @@ class FusedAdamW(FlatOptimizer):
         # profiles/r2_final/adamw_overlap_grid.txt).  0 = uncapped.
         grid = int(os.environ.get("FLEETX_ADAMW_OVERLAP_GRID", str(self.overlap_grid)))
         wide = int(os.environ.get("FLEETX_ADAMW_OVERLAP_WIDE", str(int(self.overlap_wide))))
+        # non-temporal loads / stores (1, default: each byte is touched once per step)
+        nt = int(os.environ.get("FLEETX_ADAMW_NT", "1"))
         # (running the first units -- embeddings, layer 0 -- uncapped because
         # they gate the first forward kernels measured neutral on 6.7B / 1.3B:
         # profiles/r3_adamw/head_ab.txt; every unit is capped)
@@ -504,7 +506,7 @@ class FusedAdamW(FlatOptimizer):
             st = _lib.stream()
             for i, (u, args) in enumerate(self._overlap_args):
                 if grid and i == head:
-                    k.adamw_tune(grid, 1, wide)
+                    k.adamw_tune(grid, nt, wide)
                 for adamw, mp, gp, m1, v1, pp, n, wd in args:
                     adamw(dt, mp, gp, m1, v1, pp, n, lr, b1, b2, eps, wd, 0.0, gs, fi, ds, st)
                 if self._overlap_gather:  # ZeRO: this bucket's gather follows its update
