@@ -248,13 +248,14 @@ def _train_gpu_det(rank, world, layout, overlap):
                       extra=("Distributed.comm.overlap_optimizer=%s" % overlap,))
 
 
-@pytest.mark.parametrize("name", ["pp2_1f1b", "pp2_interleaved", "zero1"])
+@pytest.mark.parametrize("name", ["pp2_1f1b", "pp2_interleaved", "zero1", "tp2", "tp2_sp"])
 def test_overlapped_update_is_bitwise_serial(name):
     """Multi-rank layouts keep the forward-overlapped update: under pipeline
     parallelism the update of step N runs on the side stream beside step
     N+1's schedule (each stage's layers wait for their own units, the
     embedding / final LN / head for the root unit before the schedule
-    starts); under ZeRO-1 each bucket's owned shard is updated on the side
+    starts); under TP / SP each rank's layers wait for their own units as
+    on one GPU; under ZeRO-1 each bucket's owned shard is updated on the side
     stream and its parameter all-gather issued right behind it, and the
     layers wait for their buckets' gathers (ZeRO-2/3 keep their own
     sharded buffer, ``parallel/sharding.py``, with a serial update).
