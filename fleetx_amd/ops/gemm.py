@@ -124,6 +124,10 @@ def out_tiles(kind, a, b, t=128):
 # 0.1-0.3 ms slower (profiles/r4_route/fwd_race_345m.txt).
 ROUTE_TUNE = os.environ.get("FLEETX_GEMM_ROUTE", "tune") == "tune"
 TUNE_KINDS = ("dgrad",)
+# Forward GEMMs follow the plan only (never raced): "plan" = an entry's
+# "route" field; "faster" = also entries without one whose planned kernel time
+# beats the vendor's by ROUTE_MARGIN (lab A/Bs); "off" = hipBLASLt.
+FWD_ROUTE = os.environ.get("FLEETX_GEMM_FWD_ROUTE", "plan")
 ROUTE_MARGIN = 0.03
 VENDOR = {}
 _ROUTE = {}
@@ -271,6 +275,23 @@ def _tuned_route(kind, a, b):
     return r
 
 
+def _planned_fwd_route(a, b):
+    key = ("fwd", a.numel() // a.shape[-1], b.shape[0], b.shape[1], a.dtype)
+    r = _ROUTE.get(key)
+    if r is not None:
+        return r
+    e = load_plan().get(("fwd", _dt_name(a.dtype), *key[1:4]))
+    r = False
+    if e is not None:
+        if "route" in e:
+            r = e["route"] == "kernel"
+        elif FWD_ROUTE == "faster" and e.get("vendor_ms") and e.get("kernel_ms"):
+            r = e["kernel_ms"] < (1.0 - ROUTE_MARGIN) * e["vendor_ms"]
+        r = r and _ok(a.reshape(-1, a.shape[-1]), b)
+    _ROUTE[key], _ROUTE_SRC[key] = r, "plan" if e is not None else "default"
+    return r
+
+
 def use(kind, a, b=None):
     """Whether GEMM ``kind`` ('fwd' | 'fwd_act' | 'dgrad' | 'dgrad_act' |
     'wgrad'; ``_act`` = with the GeLU / GeLU' epilogue) on these operands goes
@@ -286,6 +307,8 @@ def use(kind, a, b=None):
             return out_tiles(kind, a, b) >= (WGRAD_MIN_TILES if kind == "wgrad" else MIN_TILES)
         if ROUTE_TUNE and kind in TUNE_KINDS:
             return _tuned_route(kind, a, b)
+        if kind == "fwd" and FWD_ROUTE != "off":
+            return _planned_fwd_route(a, b)
         return False
     return True
 

@@ -12,4 +12,4 @@ CTRS2="GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_L
 timeout -s KILL 120 rocprofv3 --pmc $CTRS2 -d $O/pmc2 -o pmc -- python3 tools/bench_wgrad_stride.py > $O/pmc2.log 2>&1 || { tail -5 $O/pmc2.log; exit 1; }
 db=$(find $O/pmc2 -name "*.db" | head -1)
 python3 tools/pmc_summary.py "$db" --filter gemm5 > $O/pmc2_summary.txt 2>&1
-cat $O/pmc1_summary.txt $O/pmc2_summary.txt | head -60
+cat $O/pmc1_summary.txt $O/pmc2_summary.txt
