@@ -36,6 +36,9 @@ namespace {
 
 constexpr float LOG2E = 1.4426950408889634f;
 #define FA_DKDV_QT 32  // query rows per dK/dV tile
+#ifndef FA_DKDV64_QT
+#define FA_DKDV64_QT 64  // query rows per tile of the 64-keys-per-wave dK/dV kernel
+#endif
 #ifndef FA_RESCALE_THR
 #define FA_RESCALE_THR 8.0f  // log2 units; 0 = rescale on every growth
 #endif
@@ -1059,6 +1062,249 @@ __device__ __forceinline__ void dkdv_body(const AttnParams& P, char* smem) {
   }
 }
 
+// ============================================================================
+// backward dK/dV, one wave per SIMD: WG = 4 waves x 64 keys = 256 keys.
+// Each wave owns two 32-key blocks, so every Q / dO fragment read from LDS
+// (row form for S and dP, transposed form for dK and dV) feeds two MFMAs
+// instead of one.  That is 40 % less LDS traffic per FLOP than dkdv_body,
+// which is LDS-bound at two waves per SIMD.  The dK / dV accumulators of both
+// blocks (256 registers) and the K fragments (64) need the whole 512-register
+// file, so one workgroup runs per CU and V is read from an LDS image of the
+// workgroup's 256 rows.  Same element math and dropout hash as dkdv_body
+// (bitwise-equal results).
+// ============================================================================
+template <typename T, int D, bool CAUSAL, bool DROP, bool KB, int QT>
+__device__ __forceinline__ void dkdv64_body(const AttnParams& P, char* smem) {
+  constexpr int NW = 4;
+  constexpr int KR = 64 * NW;  // keys per workgroup
+  constexpr int TB = QT * D * 2;
+  constexpr int BUF = 2 * TB + 2 * QT * 4;
+  char* vs = smem + 2 * BUF;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  Frag<D> F;
+  F.init(lane);
+  const int nk = (P.Sk + KR - 1) / KR;
+  const int nblk = nk * P.B * P.H;
+  const int lid = xcd_remap(blockIdx.x, nblk);
+  int bh, kblock;
+  if constexpr (CAUSAL) {
+    lpt_order(lid, nk, P.B * P.H, bh, kblock);
+  } else {
+    bh = lid / nk;
+    kblock = lid % nk;
+  }
+  const int b = bh / P.H, hd = bh % P.H;
+  const uint16_t* qp = P.q + b * P.sq_b + hd * P.sq_h;
+  const uint16_t* kp = P.k + b * P.sk_b + hd * P.sk_h;
+  const uint16_t* vp = P.v + b * P.sv_b + hd * P.sv_h;
+  const uint16_t* dop = P.dout + b * P.so_b + hd * P.so_h;
+  int kv_len = P.Sk;
+  if (P.kv_lens) kv_len = min(kv_len, P.kv_lens[b]);
+
+  const int wk0 = kblock * KR + w * 64;
+  int ki[2];
+  float kb2[2];
+  short8 kf[2][D / 16];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    ki[kb] = wk0 + 32 * kb + (lane & 31);
+    kb2[kb] = ki[kb] >= kv_len ? -INFINITY
+                               : (KB ? P.kbias[(long)b * P.kb_b + ki[kb]] * LOG2E : 0.f);
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      if (ki[kb] < P.Sk && 16 * s + 8 * h < P.dval)
+        kf[kb][s] = *reinterpret_cast<const short8*>(kp + (long)ki[kb] * P.sk_s + 16 * s + 8 * h);
+      else
+        kf[kb][s] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  Glds<D, KR, NW>::load(vp, P.sv_s, kblock * KR, P.Sk, vs, w, lane, P.dval);
+  floatx16 dkacc[2][D / 32], dvacc[2][D / 32];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dkacc[kb][dt][i] = dvacc[kb][dt][i] = 0.f;
+  const float sl2 = P.scale * LOG2E;
+  const uint32_t cb = DROP ? attn_cb(P, bh) : 0u;
+
+  const int q_begin = CAUSAL ? (kblock * KR / QT) * QT : 0;
+  const int ntiles = P.Sq > q_begin ? (P.Sq - q_begin + QT - 1) / QT : 0;
+  float nl = INFINITY, nd = 0.f;
+  auto rowconst_load = [&](int qb) {
+    if (tid < QT) {
+      const int q = qb + tid;
+      nl = q < P.Sq ? P.lse[(long)bh * P.Sq + q] * LOG2E : INFINITY;
+      nd = q < P.Sq ? P.delta[(long)bh * P.Sq + q] : 0.f;
+    }
+  };
+  auto rowconst_store = [&](char* buf) {
+    if (tid < QT) {
+      float* c = reinterpret_cast<float*>(buf + 2 * TB);
+      c[tid] = nl;
+      c[QT + tid] = nd;
+    }
+  };
+  GldsStream<D, QT, NW> qld, gld;
+  qld.init(qp, P.sq_s, P.Sq, w, lane, P.dval);
+  gld.init(dop, P.so_s, P.Sq, w, lane, P.dval);
+  if (ntiles > 0) {
+    rowconst_load(q_begin);
+    qld.load(q_begin, smem, lane);
+    gld.load(q_begin, smem + TB, lane);
+    rowconst_store(smem);
+  }
+  glds_wait();
+  __syncthreads();
+
+  for (int it = 0; it < ntiles; ++it) {
+    const int qb = q_begin + it * QT;
+    const char* cur = smem + (it & 1) * BUF;
+    char* nxt = smem + ((it & 1) ^ 1) * BUF;
+    const bool more = it + 1 < ntiles;
+    if (more) {
+      rowconst_load(qb + QT);
+      qld.load(qb + QT, nxt, lane);
+      gld.load(qb + QT, nxt + TB, lane);
+    }
+    const char* qt = cur;
+    const char* gt = cur + TB;
+    const float* lse_s = reinterpret_cast<const float*>(cur + 2 * TB);
+    const float* dl_s = lse_s + QT;
+    if (wk0 < P.Sk && !(CAUSAL && qb + QT - 1 < wk0)) {
+#pragma unroll 1
+      for (int t = 0; t < QT / 32; ++t) {
+        const int q0 = qb + 32 * t;
+        if (CAUSAL && q0 + 31 < wk0) continue;
+        uint32_t keep[2] = {0u, 0u};
+        if (DROP) {
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; i += 2) {
+              const int q = q0 + crow(i, h);
+              const uint32_t mine =
+                  lowbias32((((uint32_t)(q + (lane & 1))) << 16 | ((uint32_t)ki[kb] >> 1)) ^ cb);
+              const uint32_t other = dpp_swap1(mine);
+              const uint32_t hq = (lane & 1) ? other : mine;
+              const uint32_t hq1 = (lane & 1) ? mine : other;
+              const uint32_t r0 = (lane & 1) ? (hq >> 16) : (hq & 0xffffu);
+              const uint32_t r1 = (lane & 1) ? (hq1 >> 16) : (hq1 & 0xffffu);
+              keep[kb] |= (r0 >= P.thr ? 1u : 0u) << i;
+              keep[kb] |= (r1 >= P.thr ? 1u : 0u) << (i + 1);
+            }
+        }
+        floatx16 sacc[2], dpacc[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) sacc[kb][i] = dpacc[kb][i] = 0.f;
+        if (CAUSAL && __builtin_expect(q0 < wk0 + 63, 0)) {
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              if (ki[kb] > q0 + crow(i, h)) sacc[kb][i] = -INFINITY;
+        }
+        // fragments one k-step ahead, no further: the compiler would otherwise
+        // hoist every k-step's LDS reads to the top (64+ registers) and spill
+        short8 qr = F.row(qt, t, 0), gr = F.row(gt, t, 0);
+        short8 v0 = F.row(vs, 2 * w, 0), v1 = F.row(vs, 2 * w + 1, 0);
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s) {
+          asm volatile("" ::: "memory");
+          short8 nq = qr, ng = gr, nv0 = v0, nv1 = v1;
+          if (s + 1 < D / 16) {
+            nq = F.row(qt, t, s + 1);
+            ng = F.row(gt, t, s + 1);
+            nv0 = F.row(vs, 2 * w, s + 1);
+            nv1 = F.row(vs, 2 * w + 1, s + 1);
+          }
+          sacc[0] = mfma<T>(qr, kf[0][s], sacc[0]);
+          sacc[1] = mfma<T>(qr, kf[1][s], sacc[1]);
+          dpacc[0] = mfma<T>(gr, v0, dpacc[0]);
+          dpacc[1] = mfma<T>(gr, v1, dpacc[1]);
+          qr = nq; gr = ng; v0 = nv0; v1 = nv1;
+        }
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          short8 pf[2], df[2];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int i = 8 * ss + j;
+            const int ql_ = 32 * t + crow(i, h);
+            const float lse_q = lse_s[ql_], dl_q = dl_s[ql_];
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+              const float p = fexp2(__builtin_fmaf(sacc[kb][i], sl2, kb2[kb] - lse_q));
+              if (DROP) {
+                const float z = ((keep[kb] >> i) & 1u) ? P.drop_scale : 0.f;
+                pf[kb][j] = cvt16<T>(p * z);
+                df[kb][j] = cvt16<T>(p * (dpacc[kb][i] * z - dl_q));
+              } else {
+                pf[kb][j] = cvt16<T>(p);
+                df[kb][j] = cvt16<T>(p * (dpacc[kb][i] - dl_q));
+              }
+            }
+          }
+          v4s glo[D / 32], ghi[D / 32];
+          F.tr_issue(gt, t, ss, glo, ghi);
+          tr_wait(glo, ghi);
+#pragma unroll
+          for (int dt = 0; dt < D / 32; ++dt) {
+            const short8 g8 = tr_join(glo[dt], ghi[dt]);
+            dvacc[0][dt] = mfma<T>(g8, pf[0], dvacc[0][dt]);
+            dvacc[1][dt] = mfma<T>(g8, pf[1], dvacc[1][dt]);
+          }
+          v4s qlo[D / 32], qhi[D / 32];
+          F.tr_issue(qt, t, ss, qlo, qhi);
+          tr_wait(qlo, qhi);
+#pragma unroll
+          for (int dt = 0; dt < D / 32; ++dt) {
+            const short8 q8 = tr_join(qlo[dt], qhi[dt]);
+            dkacc[0][dt] = mfma<T>(q8, df[0], dkacc[0][dt]);
+            dkacc[1][dt] = mfma<T>(q8, df[1], dkacc[1][dt]);
+          }
+        }
+      }
+    }
+    if (more) rowconst_store(nxt);
+    glds_wait();
+    __syncthreads();
+  }
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    if (ki[kb] >= P.Sk) continue;
+    uint16_t* dkp = P.dk + b * P.sdk_b + hd * P.sdk_h + (long)ki[kb] * P.sdk_s;
+    uint16_t* dvp = P.dv + b * P.sdk_b + hd * P.sdk_h + (long)ki[kb] * P.sdk_s;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        ushort4 a, c;
+        a.x = Elt<T>::from_f(dkacc[kb][dt][4 * g + 0] * P.scale);
+        a.y = Elt<T>::from_f(dkacc[kb][dt][4 * g + 1] * P.scale);
+        a.z = Elt<T>::from_f(dkacc[kb][dt][4 * g + 2] * P.scale);
+        a.w = Elt<T>::from_f(dkacc[kb][dt][4 * g + 3] * P.scale);
+        c.x = Elt<T>::from_f(dvacc[kb][dt][4 * g + 0]);
+        c.y = Elt<T>::from_f(dvacc[kb][dt][4 * g + 1]);
+        c.z = Elt<T>::from_f(dvacc[kb][dt][4 * g + 2]);
+        c.w = Elt<T>::from_f(dvacc[kb][dt][4 * g + 3]);
+        if (dt * 32 + 8 * g + 4 * h < P.dval) {
+          *reinterpret_cast<ushort4*>(dkp + dt * 32 + 8 * g + 4 * h) = a;
+          *reinterpret_cast<ushort4*>(dvp + dt * 32 + 8 * g + 4 * h) = c;
+        }
+      }
+  }
+}
+
+template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
+__global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_k64_kernel(AttnParams P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  dkdv64_body<T, D, CAUSAL, DROP, KB, FA_DKDV64_QT>(P, smem);
+}
+
 template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1141,6 +1387,18 @@ static bool fa_pair_grid() {
   }();
   return on;
 }
+
+// The D = 128 dK/dV pass with 64 keys per wave (dkdv64_body): FLEETX_FA_DKDV64
+// or fx_fa_set_dkdv64 (1 on, 0 off; < 0 re-reads the environment)
+static int g_dkdv64 = -1;
+static bool dkdv64() {
+  if (g_dkdv64 < 0) {
+    const char* e = getenv("FLEETX_FA_DKDV64");
+    g_dkdv64 = e ? (atoi(e) != 0) : 0;
+  }
+  return g_dkdv64 != 0;
+}
+extern "C" void fx_fa_set_dkdv64(int on) { g_dkdv64 = on < 0 ? -1 : (on != 0); }
 
 static int fwd_waves() {
   static int nw = [] {
@@ -1278,6 +1536,11 @@ static int flash_bwd_t(const void* q, const void* k, const void* v, const void* 
       const size_t smem = 2 * (2 * 64 * D * 2 + 2 * 64 * 4);
       FA_DISPATCH(fa_bwd_dkdv_q64v_kernel, D, causal, p > 0.f, kbias != nullptr, nk * B * H,
                   smem, st, P);
+    } else if (dkdv64()) {
+      // 64 keys per wave, one workgroup of 256 keys per CU
+      const size_t smem = 2 * (2 * FA_DKDV64_QT * D * 2 + 2 * FA_DKDV64_QT * 4) + 256 * D * 2;
+      FA_DISPATCH_D(fa_bwd_dkdv_k64_kernel, 128, causal, p > 0.f, kbias != nullptr,
+                    (Sk + 255) / 256 * B * H, smem, st, P);
     } else {
       const size_t smem = 2 * (2 * FA_DKDV_QT * D * 2 + 2 * FA_DKDV_QT * 4) + 128 * D * 2;
       FA_DISPATCH(fa_bwd_dkdv_kernel, D, causal, p > 0.f, kbias != nullptr, nk * B * H, smem,
