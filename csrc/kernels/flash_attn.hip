@@ -818,6 +818,213 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_kernel(AttnParams P) {
   }
 }
 
+// ============================================================================
+// backward dQ, one wave per SIMD: WG = 4 waves x 64 queries = 256 queries.
+// Each wave owns two 32-query blocks, so every K / V fragment read from LDS
+// (row form for S^T and dP^T, transposed K for dQ) feeds two MFMAs.  Q and dO
+// of both blocks stay in registers (128), the dQ accumulators take 128 more:
+// one workgroup per CU.  Same element math and dropout hash as
+// fa_bwd_dq_kernel (bitwise-equal dQ and delta).
+// ============================================================================
+template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
+__global__ __launch_bounds__(256, 1) void fa_bwd_dq64_kernel(AttnParams P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NW = 4, KV = 64, TB = KV * D * 2, QB = 64 * NW;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  Frag<D> F;
+  F.init(lane);
+  const int nq = (P.Sq + QB - 1) / QB;
+  const int nblk = nq * P.B * P.H;
+  const int lid = xcd_remap(blockIdx.x, nblk);
+  int bh, qblock;
+  if constexpr (CAUSAL) {
+    int rank;
+    lpt_order(lid, nq, P.B * P.H, bh, rank);
+    qblock = nq - 1 - rank;
+  } else {
+    bh = lid / nq;
+    qblock = lid % nq;
+  }
+  const int b = bh / P.H, hd = bh % P.H;
+  const uint16_t* qp = P.q + b * P.sq_b + hd * P.sq_h;
+  const uint16_t* kp = P.k + b * P.sk_b + hd * P.sk_h;
+  const uint16_t* vp = P.v + b * P.sv_b + hd * P.sv_h;
+  const uint16_t* dop = P.dout + b * P.so_b + hd * P.so_h;
+  int kv_len = P.Sk;
+  if (P.kv_lens) kv_len = min(kv_len, P.kv_lens[b]);
+
+  const int wq0 = qblock * QB + w * 64;
+  int qi[2];
+  float lse2[2], dlt[2];
+  short8 qf[2][D / 16], gf[2][D / 16];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    qi[a] = wq0 + 32 * a + (lane & 31);
+    const bool qvalid = qi[a] < P.Sq;
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      if (qvalid && 16 * s + 8 * h < P.dval) {
+        qf[a][s] = *reinterpret_cast<const short8*>(qp + (long)qi[a] * P.sq_s + 16 * s + 8 * h);
+        gf[a][s] = *reinterpret_cast<const short8*>(dop + (long)qi[a] * P.so_s + 16 * s + 8 * h);
+      } else {
+        qf[a][s] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
+        gf[a][s] = qf[a][s];
+      }
+    }
+    lse2[a] = qvalid ? P.lse[(long)bh * P.Sq + qi[a]] * LOG2E : INFINITY;
+  }
+  const float sl2 = P.scale * LOG2E;
+  const uint32_t cb = DROP ? attn_cb(P, bh) : 0u;
+
+  int kv_end = kv_len;
+  if (CAUSAL) kv_end = min(kv_end, (qblock + 1) * QB);
+  const int ntiles = (kv_end + KV - 1) / KV;
+
+  floatx16 dqacc[2][D / 32];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dqacc[a][dt][i] = 0.f;
+
+  GldsStream<D, KV, NW> kld, vld;
+  kld.init(kp, P.sk_s, kv_end, w, lane, P.dval);
+  vld.init(vp, P.sv_s, kv_end, w, lane, P.dval);
+  if (ntiles > 0) {
+    kld.load(0, smem, lane);
+    vld.load(0, smem + 2 * TB, lane);
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const bool qvalid = qi[a] < P.Sq;
+    float part = 0.f;
+    if (qvalid) {
+      const uint16_t* orow = P.o + b * P.so_b + hd * P.so_h + (long)qi[a] * P.so_s;
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        if (16 * s + 8 * h >= P.dval) continue;
+        float ov[8], gv[8];
+        load8<T>(orow + 16 * s + 8 * h, ov);
+        unpack8<T>(__builtin_bit_cast(uint4, gf[a][s]), gv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) part += ov[j] * gv[j];
+      }
+    }
+    part += __shfl_xor(part, 32, 64);
+    dlt[a] = qvalid ? part : 0.f;
+    if (qvalid && h == 0) P.delta[(long)bh * P.Sq + qi[a]] = dlt[a];
+  }
+  glds_wait();
+  __syncthreads();
+
+  for (int it = 0; it < ntiles; ++it) {
+    const int cur = it & 1;
+    const char* kt = smem + cur * TB;
+    const char* vt = smem + 2 * TB + cur * TB;
+    const bool more = it + 1 < ntiles;
+    if (more) {
+      kld.load((it + 1) * KV, smem + (cur ^ 1) * TB, lane);
+      vld.load((it + 1) * KV, smem + 2 * TB + (cur ^ 1) * TB, lane);
+    }
+    const int kb = it * KV;
+    if (wq0 < P.Sq && !(CAUSAL && kb > wq0 + 63)) {
+      const bool need_mask = (CAUSAL && kb + KV - 1 > wq0) || (kb + KV > kv_len);
+      const bool half2 = (kb + 32 < kv_len && !(CAUSAL && kb + 32 > wq0 + 63));
+#pragma unroll 1
+      for (int t = 0; t < 2; ++t) {
+        if (t == 1 && !half2) continue;
+        floatx16 sacc[2], dpacc[2];
+        short8 dfs[2][2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) sacc[a][i] = dpacc[a][i] = 0.f;
+        short8 kr = F.row(kt, t, 0), vr = F.row(vt, t, 0);
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s) {
+          asm volatile("" ::: "memory");
+          short8 nk = kr, nv = vr;
+          if (s + 1 < D / 16) {
+            nk = F.row(kt, t, s + 1);
+            nv = F.row(vt, t, s + 1);
+          }
+          sacc[0] = mfma<T>(kr, qf[0][s], sacc[0]);
+          sacc[1] = mfma<T>(kr, qf[1][s], sacc[1]);
+          dpacc[0] = mfma<T>(vr, gf[0][s], dpacc[0]);
+          dpacc[1] = mfma<T>(vr, gf[1][s], dpacc[1]);
+          kr = nk; vr = nv;
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          if constexpr (KB)
+            key_bias_add1(sacc[a], P.kbias + (long)b * P.kb_b + kb + 32 * t, h, sl2);
+          if (__builtin_expect(need_mask, 0)) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int key = kb + 32 * t + crow(i, h);
+              if ((CAUSAL && key > qi[a]) || key >= kv_len) sacc[a][i] = -INFINITY;
+            }
+          }
+          const float sc = KB ? 1.f : sl2;
+          // dS straight to 16-bit: the fp32 S / dP tiles die here
+#pragma unroll
+          for (int i = 0; i < 16; i += 2) {
+            const float p0 = fexp2(__builtin_fmaf(sacc[a][i], sc, -lse2[a]));
+            const float p1 = fexp2(__builtin_fmaf(sacc[a][i + 1], sc, -lse2[a]));
+            float dp0 = dpacc[a][i], dp1 = dpacc[a][i + 1];
+            float d0, d1;
+            if (DROP) {
+              const int key = kb + 32 * t + crow(i, h);
+              const uint32_t hh = lowbias32((((uint32_t)qi[a]) << 16 | ((uint32_t)key >> 1)) ^ cb);
+              dp0 = ((hh & 0xffffu) >= P.thr) ? dp0 : 0.f;
+              dp1 = ((hh >> 16) >= P.thr) ? dp1 : 0.f;
+              d0 = p0 * __builtin_fmaf(dp0, P.drop_scale, -dlt[a]);
+              d1 = p1 * __builtin_fmaf(dp1, P.drop_scale, -dlt[a]);
+            } else {
+              d0 = p0 * (dp0 - dlt[a]);
+              d1 = p1 * (dp1 - dlt[a]);
+            }
+            dfs[a][i >> 3][i & 7] = cvt16<T>(d0);
+            dfs[a][i >> 3][(i & 7) + 1] = cvt16<T>(d1);
+          }
+        }
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          v4s klo[D / 32], khi[D / 32];
+          F.tr_issue(kt, t, ss, klo, khi);
+          tr_wait(klo, khi);
+#pragma unroll
+          for (int dt = 0; dt < D / 32; ++dt) {
+            const short8 k8 = tr_join(klo[dt], khi[dt]);
+            dqacc[0][dt] = mfma<T>(k8, dfs[0][ss], dqacc[0][dt]);
+            dqacc[1][dt] = mfma<T>(k8, dfs[1][ss], dqacc[1][dt]);
+          }
+        }
+      }
+    }
+    glds_wait();
+    __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    if (qi[a] >= P.Sq) continue;
+    uint16_t* dqp = P.dq + b * P.sdq_b + hd * P.sdq_h + (long)qi[a] * P.sdq_s;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        ushort4 o;
+        o.x = Elt<T>::from_f(dqacc[a][dt][4 * g + 0] * P.scale);
+        o.y = Elt<T>::from_f(dqacc[a][dt][4 * g + 1] * P.scale);
+        o.z = Elt<T>::from_f(dqacc[a][dt][4 * g + 2] * P.scale);
+        o.w = Elt<T>::from_f(dqacc[a][dt][4 * g + 3] * P.scale);
+        if (dt * 32 + 8 * g + 4 * h < P.dval)
+          *reinterpret_cast<ushort4*>(dqp + dt * 32 + 8 * g + 4 * h) = o;
+      }
+  }
+}
+
 // swap a 32-bit value with the neighbouring lane (lane ^ 1) through DPP
 __device__ __forceinline__ uint32_t dpp_swap1(uint32_t v) {
   // quad_perm [1, 0, 3, 2]
@@ -1227,35 +1434,36 @@ __device__ __forceinline__ void dkdv64_body(const AttnParams& P, char* smem) {
           dpacc[1] = mfma<T>(gr, v1, dpacc[1]);
           qr = nq; gr = ng; v0 = nv0; v1 = nv1;
         }
+        // P o Z and dS of both key blocks to 16-bit first: the fp32 S / dP
+        // tiles (64 registers) die before the fragment reads of the MFMA phase
+        short8 pf[2][2], df[2][2];
 #pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          short8 pf[2], df[2];
+        for (int i = 0; i < 16; ++i) {
+          const int ql_ = 32 * t + crow(i, h);
+          const float lse_q = lse_s[ql_], dl_q = dl_s[ql_];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int i = 8 * ss + j;
-            const int ql_ = 32 * t + crow(i, h);
-            const float lse_q = lse_s[ql_], dl_q = dl_s[ql_];
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb) {
-              const float p = fexp2(__builtin_fmaf(sacc[kb][i], sl2, kb2[kb] - lse_q));
-              if (DROP) {
-                const float z = ((keep[kb] >> i) & 1u) ? P.drop_scale : 0.f;
-                pf[kb][j] = cvt16<T>(p * z);
-                df[kb][j] = cvt16<T>(p * (dpacc[kb][i] * z - dl_q));
-              } else {
-                pf[kb][j] = cvt16<T>(p);
-                df[kb][j] = cvt16<T>(p * (dpacc[kb][i] - dl_q));
-              }
+          for (int kb = 0; kb < 2; ++kb) {
+            const float p = fexp2(__builtin_fmaf(sacc[kb][i], sl2, kb2[kb] - lse_q));
+            if (DROP) {
+              const float z = ((keep[kb] >> i) & 1u) ? P.drop_scale : 0.f;
+              pf[kb][i >> 3][i & 7] = cvt16<T>(p * z);
+              df[kb][i >> 3][i & 7] = cvt16<T>(p * (dpacc[kb][i] * z - dl_q));
+            } else {
+              pf[kb][i >> 3][i & 7] = cvt16<T>(p);
+              df[kb][i >> 3][i & 7] = cvt16<T>(p * (dpacc[kb][i] - dl_q));
             }
           }
+        }
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
           v4s glo[D / 32], ghi[D / 32];
           F.tr_issue(gt, t, ss, glo, ghi);
           tr_wait(glo, ghi);
 #pragma unroll
           for (int dt = 0; dt < D / 32; ++dt) {
             const short8 g8 = tr_join(glo[dt], ghi[dt]);
-            dvacc[0][dt] = mfma<T>(g8, pf[0], dvacc[0][dt]);
-            dvacc[1][dt] = mfma<T>(g8, pf[1], dvacc[1][dt]);
+            dvacc[0][dt] = mfma<T>(g8, pf[0][ss], dvacc[0][dt]);
+            dvacc[1][dt] = mfma<T>(g8, pf[1][ss], dvacc[1][dt]);
           }
           v4s qlo[D / 32], qhi[D / 32];
           F.tr_issue(qt, t, ss, qlo, qhi);
@@ -1263,8 +1471,8 @@ __device__ __forceinline__ void dkdv64_body(const AttnParams& P, char* smem) {
 #pragma unroll
           for (int dt = 0; dt < D / 32; ++dt) {
             const short8 q8 = tr_join(qlo[dt], qhi[dt]);
-            dkacc[0][dt] = mfma<T>(q8, df[0], dkacc[0][dt]);
-            dkacc[1][dt] = mfma<T>(q8, df[1], dkacc[1][dt]);
+            dkacc[0][dt] = mfma<T>(q8, df[0][ss], dkacc[0][dt]);
+            dkacc[1][dt] = mfma<T>(q8, df[1][ss], dkacc[1][dt]);
           }
         }
       }
@@ -1399,6 +1607,17 @@ static bool dkdv64() {
   return g_dkdv64 != 0;
 }
 extern "C" void fx_fa_set_dkdv64(int on) { g_dkdv64 = on < 0 ? -1 : (on != 0); }
+// The D = 128 dQ pass with 64 queries per wave (fa_bwd_dq64_kernel): FLEETX_FA_DQ64
+// or fx_fa_set_dq64 (same convention)
+static int g_dq64 = -1;
+static bool dq64() {
+  if (g_dq64 < 0) {
+    const char* e = getenv("FLEETX_FA_DQ64");
+    g_dq64 = e ? (atoi(e) != 0) : 0;
+  }
+  return g_dq64 != 0;
+}
+extern "C" void fx_fa_set_dq64(int on) { g_dq64 = on < 0 ? -1 : (on != 0); }
 
 static int fwd_waves() {
   static int nw = [] {
@@ -1518,6 +1737,9 @@ static int flash_bwd_t(const void* q, const void* k, const void* v, const void* 
     if (D == 96 && waves_for(Sq) == 3) {
       const int nq = (Sq + 95) / 96;
       FA_DISPATCH_NW(fa_bwd_dq_kernel, 96, 3, causal, drop, kb, nq * B * H, smem, st, P);
+    } else if (D == 128 && dq64()) {
+      FA_DISPATCH_D(fa_bwd_dq64_kernel, 128, causal, drop, kb, (Sq + 255) / 256 * B * H, smem,
+                    st, P);
     } else {
       const int nq = (Sq + 127) / 128;
       FA_DISPATCH(fa_bwd_dq_kernel, D, causal, drop, kb, nq * B * H, smem, st, P);

@@ -1,8 +1,9 @@
-"""The 64-keys-per-wave dK/dV pass (``flash_attn.hip`` ``dkdv64_body``, D = 128,
-FLEETX_FA_DKDV64) against the 32-keys-per-wave pass it replaces and against
-the fp32 reference.  Both run the same MFMA sequence per key block (32-query
-slices in order), so dK / dV must agree bitwise; dQ is computed by the
-unchanged dQ pass.  Shapes cover a key tail (Sk not a multiple of the 256-key
+"""The one-wave-per-SIMD backward passes of ``flash_attn.hip`` (D = 128): dK/dV
+with 64 keys per wave (``dkdv64_body``, FLEETX_FA_DKDV64) and dQ with 64
+queries per wave (``fa_bwd_dq64_kernel``, FLEETX_FA_DQ64), against the
+32-per-wave passes they replace and against the fp32 reference.  Each runs
+the same MFMA sequence per 32-row block as the pass it replaces, so dQ / dK /
+dV must agree bitwise.  Shapes cover a key tail (Sk not a multiple of the 256-key
 workgroup), causal + dropout, key lengths and fp16."""
 import pytest
 import torch
@@ -40,17 +41,20 @@ def test_dkdv64_bitwise_and_reference(case):
         kw["kv_lens"] = torch.tensor([333, 600], device=DEV, dtype=torch.int32)
     try:
         k_.fa_set_dkdv64(0)
+        k_.fa_set_dq64(0)
         base = _grads(ops, q, k, v, g, **kw)
         k_.fa_set_dkdv64(1)
+        k_.fa_set_dq64(1)
         new = _grads(ops, q, k, v, g, **kw)
     finally:
         k_.fa_set_dkdv64(-1)
+        k_.fa_set_dq64(-1)
     torch.cuda.synchronize()
-    assert torch.equal(new[0], base[0])
+    assert torch.equal(new[0], base[0]), (new[0].float() - base[0].float()).abs().max()
     assert torch.equal(new[1], base[1]), (new[1].float() - base[1].float()).abs().max()
     assert torch.equal(new[2], base[2]), (new[2].float() - base[2].float()).abs().max()
     qr, kr, vr = [t.detach().float().requires_grad_() for t in (q, k, v)]
     ref = ops.attention_reference(qr, kr, vr, **kw)
     ref.backward(g.float())
-    for a, r in ((new[1], kr.grad), (new[2], vr.grad)):
+    for a, r in ((new[0], qr.grad), (new[1], kr.grad), (new[2], vr.grad)):
         assert _rel(a, r) < 3e-2, _rel(a, r)
