@@ -36,6 +36,9 @@ namespace {
 
 constexpr float LOG2E = 1.4426950408889634f;
 #define FA_DKDV_QT 32  // query rows per dK/dV tile
+#ifndef FA_DKDV_V128_QT
+#define FA_DKDV_V128_QT 32  // query rows per tile of the D = 128 V-in-registers dK/dV pass
+#endif
 #ifndef FA_DKDV64_QT
 #define FA_DKDV64_QT 64  // query rows per tile of the 64-keys-per-wave dK/dV kernel
 #endif
@@ -1052,6 +1055,7 @@ __device__ __forceinline__ uint32_t dpp_swap1(uint32_t v) {
 // 128-row LDS image (keeps two workgroups per CU at QT = 64).
 template <typename T, int D, bool CAUSAL, bool DROP, bool KB, int QT, bool VREG, int NW = 4>
 __device__ __forceinline__ void dkdv_body(const AttnParams& P, char* smem) {
+  constexpr bool LEAN = D == 128 && VREG;
   constexpr int KR = 32 * NW;  // keys per workgroup
   constexpr int TB = QT * D * 2;
   // one buffer: [Q tile][dO tile][lse2 QT floats][delta QT floats]; then V rows
@@ -1197,17 +1201,57 @@ __device__ __forceinline__ void dkdv_body(const AttnParams& P, char* smem) {
           for (int i = 0; i < 16; ++i)
             if (ki > q0 + crow(i, h)) sacc[i] = -INFINITY;
         }
+        if constexpr (LEAN) {
+          // D = 128 with V in registers: fragments one k-step ahead only (the
+          // compiler would hoist all of them) so the 2-wave budget holds
+          short8 qr = F.row(qt, t, 0), gr = F.row(gt, t, 0);
 #pragma unroll
-        for (int s = 0; s < D / 16; ++s) {
-          sacc = mfma<T>(F.row(qt, t, s), kf[s], sacc);
-          if constexpr (VREG) dpacc = mfma<T>(F.row(gt, t, s), vf[s], dpacc);
-          else dpacc = mfma<T>(F.row(gt, t, s), F.row(vs, w, s), dpacc);
+          for (int s = 0; s < D / 16; ++s) {
+            asm volatile("" ::: "memory");
+            short8 nq = qr, ng = gr;
+            if (s + 1 < D / 16) {
+              nq = F.row(qt, t, s + 1);
+              ng = F.row(gt, t, s + 1);
+            }
+            sacc = mfma<T>(qr, kf[s], sacc);
+            dpacc = mfma<T>(gr, vf[s], dpacc);
+            qr = nq; gr = ng;
+          }
+        } else {
+#pragma unroll
+          for (int s = 0; s < D / 16; ++s) {
+            sacc = mfma<T>(F.row(qt, t, s), kf[s], sacc);
+            if constexpr (VREG) dpacc = mfma<T>(F.row(gt, t, s), vf[s], dpacc);
+            else dpacc = mfma<T>(F.row(gt, t, s), F.row(vs, w, s), dpacc);
+          }
+        }
+        // LEAN: P o Z and dS of the whole slice to 16-bit before the MFMA
+        // phase, so the fp32 S / dP tiles die first
+        short8 pfa[LEAN ? 2 : 1], dfa[LEAN ? 2 : 1];
+        if constexpr (LEAN) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int ql_ = 32 * t + crow(i, h);
+            const float p = fexp2(__builtin_fmaf(sacc[i], sl2, kb2 - lse_s[ql_]));
+            if (DROP) {
+              const float z = ((keep >> i) & 1u) ? P.drop_scale : 0.f;
+              pfa[i >> 3][i & 7] = cvt16<T>(p * z);
+              dfa[i >> 3][i & 7] = cvt16<T>(p * (dpacc[i] * z - dl_s[ql_]));
+            } else {
+              pfa[i >> 3][i & 7] = cvt16<T>(p);
+              dfa[i >> 3][i & 7] = cvt16<T>(p * (dpacc[i] - dl_s[ql_]));
+            }
+          }
         }
         // P o Z (for dV) and dS (for dK) straight to bf16, one 8-row half at a
         // time: no fp32 copies of the tile stay live across the MFMAs
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
           short8 pf, df;
+          if constexpr (LEAN) {
+            pf = pfa[ss];
+            df = dfa[ss];
+          } else
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const int i = 8 * ss + j;
@@ -1524,6 +1568,12 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dkdv_q64v_kernel(AttnParams
   // launched for D <= 96 only (D = 128 has no registers for V; it would spill)
   if constexpr (D <= 96) dkdv_body<T, D, CAUSAL, DROP, KB, 64, true, NW>(P, smem);
 }
+// D = 128 with V in registers (FLEETX_FA_DKDV_VREG: lean register plan)
+template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_v128_kernel(AttnParams P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if constexpr (D == 128) dkdv_body<T, D, CAUSAL, DROP, KB, FA_DKDV_V128_QT, true>(P, smem);
+}
 
 AttnParams make_params(const void* q, const void* k, const void* v, const long* qs,
                        const long* ks, const long* vs, int B, int H, int Sq, int Sk, float scale,
@@ -1607,6 +1657,17 @@ static bool dkdv64() {
   return g_dkdv64 != 0;
 }
 extern "C" void fx_fa_set_dkdv64(int on) { g_dkdv64 = on < 0 ? -1 : (on != 0); }
+// The D = 128 dK/dV pass with V in registers (fa_bwd_dkdv_v128_kernel):
+// FLEETX_FA_DKDV_VREG or fx_fa_set_dkdv_vreg (same convention)
+static int g_dkdv_vreg = -1;
+static bool dkdv_vreg() {
+  if (g_dkdv_vreg < 0) {
+    const char* e = getenv("FLEETX_FA_DKDV_VREG");
+    g_dkdv_vreg = e ? (atoi(e) != 0) : 0;
+  }
+  return g_dkdv_vreg != 0;
+}
+extern "C" void fx_fa_set_dkdv_vreg(int on) { g_dkdv_vreg = on < 0 ? -1 : (on != 0); }
 // The D = 128 dQ pass with 64 queries per wave (fa_bwd_dq64_kernel): FLEETX_FA_DQ64
 // or fx_fa_set_dq64 (same convention)
 static int g_dq64 = -1;
@@ -1758,6 +1819,11 @@ static int flash_bwd_t(const void* q, const void* k, const void* v, const void* 
       const size_t smem = 2 * (2 * 64 * D * 2 + 2 * 64 * 4);
       FA_DISPATCH(fa_bwd_dkdv_q64v_kernel, D, causal, p > 0.f, kbias != nullptr, nk * B * H,
                   smem, st, P);
+    } else if (dkdv_vreg()) {
+      // D = 128, V in registers: no V image in LDS
+      const size_t smem = 2 * (2 * FA_DKDV_V128_QT * D * 2 + 2 * FA_DKDV_V128_QT * 4);
+      FA_DISPATCH_D(fa_bwd_dkdv_v128_kernel, 128, causal, p > 0.f, kbias != nullptr, nk * B * H,
+                    smem, st, P);
     } else if (dkdv64()) {
       // 64 keys per wave, one workgroup of 256 keys per CU
       const size_t smem = 2 * (2 * FA_DKDV64_QT * D * 2 + 2 * FA_DKDV64_QT * 4) + 256 * D * 2;

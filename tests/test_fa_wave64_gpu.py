@@ -3,7 +3,8 @@ with 64 keys per wave (``dkdv64_body``, FLEETX_FA_DKDV64) and dQ with 64
 queries per wave (``fa_bwd_dq64_kernel``, FLEETX_FA_DQ64), against the
 32-per-wave passes they replace and against the fp32 reference.  Each runs
 the same MFMA sequence per 32-row block as the pass it replaces, so dQ / dK /
-dV must agree bitwise.  Shapes cover a key tail (Sk not a multiple of the 256-key
+dV must agree bitwise.  ``vreg``: the 2-wave dK/dV pass with V in registers
+(``fa_bwd_dkdv_v128_kernel``, FLEETX_FA_DKDV_VREG).  Shapes cover a key tail (Sk not a multiple of the 256-key
 workgroup), causal + dropout, key lengths and fp16."""
 import pytest
 import torch
@@ -24,8 +25,9 @@ def _grads(ops, q, k, v, g, **kw):
     return q.grad, k.grad, v.grad
 
 
+@pytest.mark.parametrize("variant", ["wave64", "vreg"])
 @pytest.mark.parametrize("case", ["causal_drop", "causal", "full_kvlens", "causal_fp16"])
-def test_dkdv64_bitwise_and_reference(case):
+def test_dkdv64_bitwise_and_reference(case, variant):
     from fleetx_amd import ops
     from fleetx_amd.ops import _lib
     k_ = _lib.kernels()
@@ -42,13 +44,18 @@ def test_dkdv64_bitwise_and_reference(case):
     try:
         k_.fa_set_dkdv64(0)
         k_.fa_set_dq64(0)
+        k_.fa_set_dkdv_vreg(0)
         base = _grads(ops, q, k, v, g, **kw)
-        k_.fa_set_dkdv64(1)
-        k_.fa_set_dq64(1)
+        if variant == "wave64":
+            k_.fa_set_dkdv64(1)
+            k_.fa_set_dq64(1)
+        else:
+            k_.fa_set_dkdv_vreg(1)
         new = _grads(ops, q, k, v, g, **kw)
     finally:
         k_.fa_set_dkdv64(-1)
         k_.fa_set_dq64(-1)
+        k_.fa_set_dkdv_vreg(-1)
     torch.cuda.synchronize()
     assert torch.equal(new[0], base[0]), (new[0].float() - base[0].float()).abs().max()
     assert torch.equal(new[1], base[1]), (new[1].float() - base[1].float()).abs().max()
