@@ -275,9 +275,12 @@ def _tuned_route(kind, a, b):
     return r
 
 
+_FWD_ROUTE = {}  # forward routes from the plan (kept apart from the raced table)
+
+
 def _planned_fwd_route(a, b):
     key = ("fwd", a.numel() // a.shape[-1], b.shape[0], b.shape[1], a.dtype)
-    r = _ROUTE.get(key)
+    r = _FWD_ROUTE.get(key)
     if r is not None:
         return r
     e = load_plan().get(("fwd", _dt_name(a.dtype), *key[1:4]))
@@ -288,7 +291,7 @@ def _planned_fwd_route(a, b):
         elif FWD_ROUTE == "faster" and e.get("vendor_ms") and e.get("kernel_ms"):
             r = e["kernel_ms"] < (1.0 - ROUTE_MARGIN) * e["vendor_ms"]
         r = r and _ok(a.reshape(-1, a.shape[-1]), b)
-    _ROUTE[key], _ROUTE_SRC[key] = r, "plan" if e is not None else "default"
+    _FWD_ROUTE[key] = r
     return r
 
 

@@ -2,7 +2,7 @@
 # Round 5 end: full GPU suite + smoke + default bench on the final tree
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r5ft
+O=gpurun_out/${OUT:-r5ft}
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
