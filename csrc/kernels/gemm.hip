@@ -77,6 +77,7 @@ static int gemm_tuned_gm(int dt, int la, int lb, int epi, const GemmParams& P0, 
   P.aux = nullptr;
   P.beta = 0;
   P.sq = nullptr;
+  P.ctr = 0;
   const int tepi = f32 ? EPI_F32 : EPI_STORE;
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
@@ -112,6 +113,11 @@ static int gemm_tuned_gm(int dt, int la, int lb, int epi, const GemmParams& P0, 
 extern "C" int fx_gemm(int dt, int la, int lb, int epi, int M, int N, int K, const void* A,
                        long lda, const void* B, long ldb, void* C, long ldc, const void* bias,
                        void* aux, long ldaux, int beta, hipStream_t st, float* sq, float* ws) {
+  int ctr = 0;
+  if (epi == EPI_F32BT) {  // transposed 16-bit weight gradient: C[m][n] at C + n * ldc + m
+    epi = EPI_F32B;
+    ctr = 1;
+  }
   if (M <= 0 || N <= 0 || K < 2 * BK || K % BK) return -1;
   if (sq != nullptr && !epi_wgrad(epi)) return -5;
   if (epi == EPI_F32B && beta) return -6;  // 16-bit gradients are written, never accumulated
@@ -120,7 +126,8 @@ extern "C" int fx_gemm(int dt, int la, int lb, int epi, int M, int N, int K, con
   const long a_span = la == LAY_KC ? (long)M * lda : (long)BK * lda + M;
   const long b_span = lb == LAY_KC ? (long)N * ldb : (long)BK * ldb + N;
   if (a_span >= (1L << 31) || b_span >= (1L << 31)) return -4;
-  if ((long)M * ldc * (epi == EPI_F32 ? 4 : 2) >= (1L << 31)) return -4;
+  if ((long)(ctr ? N : M) * ldc * (epi == EPI_F32 ? 4 : 2) >= (1L << 31)) return -4;
+  if (ctr && ldc < M) return -2;
   if (aux && (long)M * ldaux * 2 >= (1L << 31)) return -4;
   GemmParams P{};
   P.A = (const uint16_t*)A;
@@ -133,6 +140,7 @@ extern "C" int fx_gemm(int dt, int la, int lb, int epi, int M, int N, int K, con
   P.beta = beta;
   P.sq = sq;
   P.ws = epi_wgrad(epi) ? ws : nullptr;
+  P.ctr = ctr;
   if (g_gm < 0) {
     const char* e = getenv("FLEETX_GEMM_GM");
     g_gm = e ? atoi(e) : 0;

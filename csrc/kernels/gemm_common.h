@@ -11,7 +11,9 @@ enum { EPI_STORE = 0, EPI_BIAS_GELU = 1, EPI_DGELU = 2, EPI_F32 = 3, EPI_BIAS_GE
        EPI_DGELU_ERF = 5,
        // weight gradient stored in 16 bits (fp32 accumulation, beta 0): the
        // bf16 gradient storage of Distributed.comm.grad_dtype
-       EPI_F32B = 6 };
+       EPI_F32B = 6,
+       // fx_gemm only: EPI_F32B with C stored transposed (GemmParams::ctr)
+       EPI_F32BT = 7 };
 
 // the fp32-accumulating weight-gradient epilogues (split-K, norm partials)
 constexpr bool epi_wgrad(int e) { return e == EPI_F32 || e == EPI_F32B; }
@@ -56,6 +58,9 @@ struct GemmParams {
   // range xcd_remap / the persistent queues deal to XCD r; the gm order runs
   // inside each rectangle.  0 = the gm order over the whole grid.
   int xm;
+  // EPI_F32B: 1 = C[m][n] is stored at C + n * ldc + m (the transposed
+  // product of a wide weight gradient, fx_gemm EPI_F32BT); unsplit launches only
+  int ctr;
 };
 
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {

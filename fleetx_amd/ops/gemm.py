@@ -29,7 +29,8 @@ import torch
 from . import _lib
 
 LAY_KC, LAY_MC = 0, 1
-EPI_STORE, EPI_BIAS_GELU, EPI_DGELU, EPI_F32, EPI_BIAS_GELU_ERF, EPI_DGELU_ERF, EPI_F32B = range(7)
+EPI_STORE, EPI_BIAS_GELU, EPI_DGELU, EPI_F32, EPI_BIAS_GELU_ERF, EPI_DGELU_ERF, EPI_F32B, \
+    EPI_F32BT = range(8)
 
 _MODE = os.environ.get("FLEETX_GEMM", "auto")
 
@@ -403,6 +404,11 @@ def linear_dgrad(dy2, w, act_input=None, act="gelu", out=None):
     return dx
 
 
+# 16-bit weight gradients wider than tall through the transposed product
+# (linear_wgrad; FLEETX_GEMM_WGRAD_T=0 keeps the plain order)
+WGRAD_T = os.environ.get("FLEETX_GEMM_WGRAD_T", "0") == "1"
+
+
 def covers_wgrad(dy2, x2):
     """Whether :func:`linear_wgrad` takes ``dy2^T x2`` (same checks as the
     kernel: 16-bit token-major operands, tokens a multiple of 64, extents of
@@ -439,9 +445,19 @@ def linear_wgrad(dy2, x2, out32, accumulate, sq=None):
     # C[N, K] = sum_m A[n, m] B[m, k]: A = dy stored [m][n], B = x stored [m][k]
     if sq is not None and (sq.dtype != torch.float32 or sq.numel() < sq_slots(N, K)):
         raise ValueError("linear_wgrad: sq needs {} fp32 slots".format(sq_slots(N, K)))
-    rc = _launch(_lib.dt_code(dy2.dtype), LAY_MC, LAY_MC, EPI_F32B if out16 else EPI_F32, N, K,
-                 M, dy2, dy2.stride(0), x2, x2.stride(0), out32, K, beta=accumulate, sq=sq,
-                 ws=_splitk_ws(N, K, M, dy2.device))
+    rc = -1
+    if out16 and N < K and WGRAD_T:
+        # wide gradient (FC2: [4096, 16384]): run the transposed product
+        # x^T dy, the FC1 operand order, and store it transposed.  The FC2 order
+        # takes 46 % more L2 misses (profiles/r5_gemm_pmc/); -7 = the shape
+        # would split along K, where only the plain order exists
+        rc = _launch(_lib.dt_code(dy2.dtype), LAY_MC, LAY_MC, EPI_F32BT, K, N, M, x2,
+                     x2.stride(0), dy2, dy2.stride(0), out32, K, sq=sq,
+                     ws=_splitk_ws(K, N, M, dy2.device))
+    if rc != 0:
+        rc = _launch(_lib.dt_code(dy2.dtype), LAY_MC, LAY_MC, EPI_F32B if out16 else EPI_F32, N,
+                     K, M, dy2, dy2.stride(0), x2, x2.stride(0), out32, K, beta=accumulate, sq=sq,
+                     ws=_splitk_ws(N, K, M, dy2.device))
     if rc == 0:
         _lib.maybe_sync()
     return rc == 0

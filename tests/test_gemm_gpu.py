@@ -490,3 +490,35 @@ def test_tile_order_codes_are_bitwise_equal(gemm, M, N, K):
     for o in outs[1:]:
         for a, c in zip(outs[0], o):
             assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("shape", [(1024, 3072, 4096), (512, 512, 2048)])
+def test_wgrad_transposed_store_matches_plain(shape):
+    """A 16-bit weight gradient wider than tall (N < K) through the transposed
+    product x^T dy with the transposed store (EPI_F32BT, ops/gemm.py
+    linear_wgrad under FLEETX_GEMM_WGRAD_T) equals the plain order bitwise,
+    and its norm partials sum to the same total.  The second shape would split
+    along K, so the kernel declines (-7) and the plain order runs."""
+    from fleetx_amd.ops import gemm as G
+    T, N, K = shape
+    torch.manual_seed(3)
+    dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
+    outs, sqs = [], []
+    old = G.WGRAD_T
+    try:
+        for on in (False, True):
+            G.WGRAD_T = on
+            out = torch.full((N, K), float("nan"), device="cuda", dtype=torch.bfloat16)
+            sq = torch.zeros(G.sq_slots(N, K), device="cuda", dtype=torch.float32)
+            assert G.linear_wgrad(dy, x, out, False, sq=sq)
+            outs.append(out)
+            sqs.append(sq)
+    finally:
+        G.WGRAD_T = old
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref = (dy.float().t() @ x.float())
+    assert _rel(outs[1], ref) < 1e-2
+    s0, s1 = float(sqs[0].double().sum()), float(sqs[1].double().sum())
+    assert abs(s0 - s1) <= 1e-5 * s0, (s0, s1)
