@@ -405,8 +405,10 @@ def linear_dgrad(dy2, w, act_input=None, act="gelu", out=None):
 
 
 # 16-bit weight gradients wider than tall through the transposed product
-# (linear_wgrad; FLEETX_GEMM_WGRAD_T=0 keeps the plain order)
-WGRAD_T = os.environ.get("FLEETX_GEMM_WGRAD_T", "0") == "1"
+# (linear_wgrad): 6.7B FC2 1365 -> 1460-1474 TF/s, step -1.1 to -2.3 ms,
+# bitwise the plain order (profiles/r5_wgrad_t/).  FLEETX_GEMM_WGRAD_T=0 keeps
+# the plain order.
+WGRAD_T = os.environ.get("FLEETX_GEMM_WGRAD_T", "1") == "1"
 
 
 def covers_wgrad(dy2, x2):
