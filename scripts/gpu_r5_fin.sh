@@ -2,7 +2,7 @@
 # Round 5 final numbers: model zoo benches, fp16, 175B-shape, ViT-g, multi-rank rehearsal
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r5fin
+O=gpurun_out/${OUT:-r5fin}
 mkdir -p $O
 run() {  # name, args...
   local name=$1; shift
