@@ -171,12 +171,37 @@ def kernel_shape(kind, M, N, K):
     return la, lb, f32, M, N, K
 
 
+# Vendor-GEMM solutions (hipBLASLt / rocBLAS, the forward and TN data-gradient
+# GEMMs that stay on the library) picked per shape by PyTorch TunableOp on an
+# MI355X for the single-GPU model zoo (scripts/gpu_r5_ar.sh).  Loaded read-only:
+# shapes missing from the file run the library default.
+# FLEETX_VENDOR_TUNE=off skips it; PYTORCH_TUNABLEOP_* set by the user win.
+VENDOR_TUNE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                "tunableop_gfx950.csv")
+
+
+def enable_vendor_tuning():
+    if os.environ.get("FLEETX_VENDOR_TUNE", "on") == "off" \
+            or any(k.startswith("PYTORCH_TUNABLEOP") for k in os.environ) \
+            or not torch.cuda.is_available() or not os.path.exists(VENDOR_TUNE_FILE):
+        return False
+    import torch.cuda.tunable as tunable
+    tunable.enable(True)
+    tunable.tuning_enable(False)
+    tunable.record_untuned_enable(False)
+    if not tunable.read_file(VENDOR_TUNE_FILE):
+        tunable.enable(False)
+        return False
+    return True
+
+
 def load_plan(path=None, force=False):
     """Read the plan (once) and preload its tile orders into the kernel
     library; returns {key: entry}.  A missing / foreign-arch plan is empty."""
     global _PLAN
     if _PLAN is not None and not force:
         return _PLAN
+    enable_vendor_tuning()
     import json
     plan = {}
     path = path or PLAN_FILE
