@@ -247,9 +247,10 @@ def main():
             "final_loss": round(lval, 4),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)
             if torch.cuda.is_available() else None,
-            # shapes the per-shape GEMM race sent to the MFMA kernel (ops/gemm.py)
-            "gemm_raced_to_kernel": sorted("%s %dx%dx%d" % k for k, v in
-                                           gemm_routes.route_table().items() if v),
+            # forward / data-gradient shapes routed to the MFMA kernel and
+            # where each route came from (shipped plan or first-call race);
+            # weight gradients follow the kind table (ops/gemm.py)
+            "gemm_kernel_routes": gemm_routes.kernel_routes(),
         }
         print(json.dumps(out), flush=True)
     if dist.is_initialized():

@@ -175,13 +175,15 @@ def kernel_shape(kind, M, N, K):
 # GEMMs that stay on the library) picked per shape by PyTorch TunableOp on an
 # MI355X for the single-GPU model zoo (scripts/gpu_r5_ar.sh).  Loaded read-only:
 # shapes missing from the file run the library default.
-# FLEETX_VENDOR_TUNE=off skips it; PYTORCH_TUNABLEOP_* set by the user win.
+# Opt-in (FLEETX_VENDOR_TUNE=on): its A/B is neutral at the 6.7B headline
+# (288.17 vs 288.16 ms, profiles/r5_vendor_tune/) and it turns TunableOp on
+# for every torch GEMM of the process; PYTORCH_TUNABLEOP_* set by the user win.
 VENDOR_TUNE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                 "tunableop_gfx950.csv")
 
 
 def enable_vendor_tuning():
-    if os.environ.get("FLEETX_VENDOR_TUNE", "on") == "off" \
+    if os.environ.get("FLEETX_VENDOR_TUNE", "off") != "on" \
             or any(k.startswith("PYTORCH_TUNABLEOP") for k in os.environ) \
             or not torch.cuda.is_available() or not os.path.exists(VENDOR_TUNE_FILE):
         return False
@@ -245,6 +247,19 @@ def plan_route(kind, M, N, K, dtype):
 def route_table():
     """{(kind, M, N, K): True if the MFMA kernel takes it} decided so far."""
     return {k[:4]: v for k, v in _ROUTE.items()}
+
+
+def kernel_routes():
+    """{"kind MxNxK": source} of every shape routed to the MFMA kernel so far
+    (data gradients: "plan" / "race"; forwards: "plan"), for the bench line."""
+    out = {}
+    for k, v in _ROUTE.items():
+        if v:
+            out["%s %dx%dx%d" % k[:4]] = _ROUTE_SRC.get(k, "default")
+    for k, v in _FWD_ROUTE.items():
+        if v:
+            out["%s %dx%dx%d" % k[:4]] = "plan"
+    return dict(sorted(out.items()))
 
 
 def route_sources():

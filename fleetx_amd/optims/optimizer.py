@@ -291,6 +291,10 @@ class FlatOptimizer:
         returns False (and changes nothing) otherwise."""
         from ..parallel.sharding import find_layer_units
         buf = self.buffer
+        if not self._overlap_capable:
+            # no side-stream update (Momentum): under ZeRO the serial update's
+            # step() then issues the parameter all-gather itself
+            return False
         if buf.device.type != "cuda" or self.offload or not hasattr(buf, "offsets"):
             return False
         if getattr(buf, "shard_stage", 0) != 0:
@@ -332,6 +336,9 @@ class FlatOptimizer:
         return True
 
     _overlap_gather = False
+    # the subclass implements _update_overlapped (which also issues the ZeRO
+    # parameter gathers when _overlap_gather is set)
+    _overlap_capable = False
 
     def _enable_sharded_overlap(self):
         """ZeRO-1 (and stage 2 under pipeline parallelism, which keeps the
@@ -430,6 +437,7 @@ class FusedAdamW(FlatOptimizer):
     """AdamW (decoupled decay) with fp32 master weights, one launch per range."""
 
     decoupled = True
+    _overlap_capable = True
 
     def __init__(self, learning_rate, buffer, grad_clip=None, weight_decay=0.01, beta1=0.9,
                  beta2=0.999, epsilon=1e-8, multi_precision=True, **kw):
@@ -491,10 +499,12 @@ class FusedAdamW(FlatOptimizer):
                     s, e, c = self.ranges[ri]
                     a, b = lo - s, hi - s
                     g = gviews[ri][a:b]
+                    wd = float(self.weight_decay if c.decay else 0.0)
+                    # AdamW: decoupled decay; Adam: L2 term (as in _update)
+                    wd_dec, l2 = (wd, 0.0) if self.decoupled else (0.0, wd)
                     args.append((self._adamw_fn(g), self._mslice(ri, a, b).data_ptr(), g.data_ptr(),
                                  self.m[ri][a:b].data_ptr(), self.v[ri][a:b].data_ptr(),
-                                 pf[lo:hi].data_ptr(), hi - lo,
-                                 float(self.weight_decay if c.decay else 0.0)))
+                                 pf[lo:hi].data_ptr(), hi - lo, wd_dec, l2))
                 units.append((u, args))
             self._overlap_args = units
             self._overlap_dev = (self.gscale.data_ptr(), self.found_inf.data_ptr(),
@@ -507,8 +517,8 @@ class FusedAdamW(FlatOptimizer):
             for i, (u, args) in enumerate(self._overlap_args):
                 if grid and i == head:
                     k.adamw_tune(grid, nt, wide)
-                for adamw, mp, gp, m1, v1, pp, n, wd in args:
-                    adamw(dt, mp, gp, m1, v1, pp, n, lr, b1, b2, eps, wd, 0.0, gs, fi, ds, st)
+                for adamw, mp, gp, m1, v1, pp, n, wd, l2 in args:
+                    adamw(dt, mp, gp, m1, v1, pp, n, lr, b1, b2, eps, wd, l2, gs, fi, ds, st)
                 if self._overlap_gather:  # ZeRO: this bucket's gather follows its update
                     self.buffer.gather_bucket_async(u)
                     continue
@@ -570,7 +580,7 @@ class FusedAdamW(FlatOptimizer):
             if not self.decoupled:
                 raise NotImplementedError("sharding_offload supports the decoupled AdamW family")
             return self._update_offloaded(lr)
-        if self._overlap_groups is not None and self.decoupled:
+        if self._overlap_groups is not None:
             return self._update_overlapped(lr)
         pf = self.buffer.param_flat
         masters = [self._mslice(ri, 0, e - s) for ri, (s, e, _) in enumerate(self.ranges)]

@@ -217,8 +217,8 @@ class Communicator:
         # several ranks on one device, where RCCL refuses to run)
         nccl = dist.get_backend(group.group if group is not None else None) == "nccl"
         force = os.environ.get("FLEETX_ONESHOT_FORCE", "0") == "1"
-        # the same on every rank (env, backend, group size): world_error_flag
-        # keys its world collective on it
+        # (world_error_flag does not key on this: communicators are created
+        # lazily and differ between pipeline stages; world_oneshot_possible)
         self.tried_oneshot = bool(oneshot and self.nranks > 1 and torch.cuda.is_available()
                                   and (nccl or force))
         if self.tried_oneshot:
@@ -280,17 +280,30 @@ def error_flag():
     return out
 
 
+def world_oneshot_possible():
+    """Whether ANY rank's communicator may take the one-shot path, decided
+    from state that is the same on every rank: the env switches, the world
+    backend and the world size.  (Which communicators a rank has created is
+    NOT rank-invariant: they are created lazily, and under pipeline
+    parallelism the first, middle and last stages reach different
+    collectives -- keying a world collective on them hangs the ranks that
+    skip it.)"""
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return False
+    if os.environ.get("FLEETX_ONESHOT", "1") != "1" or not torch.cuda.is_available():
+        return False
+    return dist.get_backend() == "nccl" or os.environ.get("FLEETX_ONESHOT_FORCE", "0") == "1"
+
+
 def world_error_flag():
     """:func:`error_flag` shared by EVERY rank (MAX over the world, 4 bytes),
-    or :func:`error_flag` alone when no communicator attempted the one-shot
-    path.  Communicators are created by the same SPMD code on every rank and
-    the attempt depends only on env / backend / group size, so whether the
-    collective runs is the same everywhere, even where a group's one-shot
-    setup failed (that rank then contributes a zero)."""
+    or :func:`error_flag` alone when no rank can take the one-shot path.
+    Whether the collective runs comes from :func:`world_oneshot_possible`
+    (env / backend / world size), so every rank enters it at the same step,
+    also ranks that never created a communicator, or whose group's one-shot
+    setup failed (they contribute a zero)."""
     err = error_flag()
-    if not any(c.tried_oneshot for c in _COMMS.values()):
-        return err
-    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+    if not world_oneshot_possible():
         return err
     dev = torch.device("cuda", torch.cuda.current_device())
     err = torch.zeros(1, dtype=torch.int32, device=dev) if err is None \

@@ -78,13 +78,15 @@ class Category:
 
 
 class Bucket:
-    __slots__ = ("start", "end", "params", "ready", "work", "launched", "shard_ranges")
+    __slots__ = ("start", "end", "params", "ready", "work", "launched", "shard_ranges",
+                 "prescaled")
 
     def __init__(self, start, end, params):
         self.start, self.end, self.params = start, end, params
         self.ready = 0
         self.work = None
         self.launched = False
+        self.prescaled = False  # 16-bit storage averaged before its collective
 
 
 def _is_gloo(g):
@@ -101,11 +103,14 @@ def _is_gloo(g):
 
 def grad16_eligible(p, fused_wgrad=True):
     """A weight whose whole gradient is ONE write of the weight-gradient GEMM
-    (fused into main_grad, not a tied weight with a second part): its gradient
-    can be stored in 16 bits straight from the GEMM's fp32 accumulators."""
+    (fused into main_grad, not a tied weight with a second part, not a
+    sequence-parallel weight whose overlapped backward accumulates it chunk by
+    chunk): its gradient can be stored in 16 bits straight from the GEMM's
+    fp32 accumulators, rounded once."""
     return (p.dim() == 2 and fused_wgrad and bool(getattr(p, "_fx_fused_wgrad_ok", False))
             and bool(getattr(p, "_fx_gemm_wgrad", False))
-            and getattr(p, "_fx_grad_parts", 1) == 1)
+            and getattr(p, "_fx_grad_parts", 1) == 1
+            and not getattr(p, "_fx_grad_chunked", False))
 
 
 def default_decay_fn(name, p):
@@ -446,6 +451,14 @@ class FlatParamGradBuffer:
     def _data_groups(self):
         return self.dp_group, self.shard_group
 
+    def _data_world(self):
+        n = 1
+        if self.dp_group is not None:
+            n *= self.dp_group.nranks
+        if self.shard_group is not None:
+            n *= self.shard_group.nranks
+        return n
+
     def _launch(self, b):
         if b.launched:
             return
@@ -461,6 +474,14 @@ class FlatParamGradBuffer:
         low = (self.reduce_dtype != seg.dtype and seg.dtype == torch.float32
                and (self.dp_group is not None or self.shard_group is not None))
         src = seg.to(self.reduce_dtype) if low else seg
+        b.prescaled = False
+        if seg.dtype != torch.float32 and self._data_world() > 1:
+            # 16-bit gradient storage is reduced in place in 16 bits: average
+            # BEFORE the sum (reference all_reduce_parameters scales the
+            # fused 16-bit grad by 1/nranks first), so the 16-bit partial
+            # sums stay at the gradient's own magnitude
+            seg.mul_(1.0 / self._data_world())
+            b.prescaled = True
         if self.shard_stage >= 1 and self.shard_group is not None:
             # reduce-scatter to the owner (in place: RCCL's recvbuff = sendbuff + rank*count);
             # dp all-reduce of the owned shard follows in finish()
@@ -498,11 +519,7 @@ class FlatParamGradBuffer:
         for b in self.buckets:
             if not b.launched:
                 self._launch(b)
-        data_world = 1
-        if self.dp_group is not None:
-            data_world *= self.dp_group.nranks
-        if self.shard_group is not None:
-            data_world *= self.shard_group.nranks
+        data_world = self._data_world()
         for b in self.buckets:
             kind, works, seg, wire = b.work
             for w in works:
@@ -511,7 +528,7 @@ class FlatParamGradBuffer:
                 seg.copy_(wire)
             if kind == "rs" and self.dp_group is not None:
                 dist.all_reduce(seg, group=self.dp_group.group)
-            if data_world > 1:
+            if data_world > 1 and not b.prescaled:
                 seg.mul_(1.0 / data_world)
         # sequence-parallel replicated params: one coalesced mp all-reduce per range
         if self.mp_group is not None:

@@ -99,6 +99,9 @@ class ColumnParallelLinear(nn.Module):
         self.weight.tp_dim = 0
         self.weight._fx_fused_wgrad_ok = True
         self.weight._fx_gemm_wgrad = True  # gradient from the wgrad GEMM (fused-norm partials)
+        # the SP-overlapped backward writes the gradient in sequence chunks
+        # (several GEMM writes): never 16-bit storage (grad16_eligible)
+        self.weight._fx_grad_chunked = self.sequence_parallel
         if bias:
             self.bias = nn.Parameter(init_full_then_slice((out_features,), 0.0, name + ".bias",
                                                           dim=0, dtype=dtype, device=device,
@@ -151,6 +154,7 @@ class RowParallelLinear(nn.Module):
         self.weight.tp_dim = 1
         self.weight._fx_fused_wgrad_ok = True
         self.weight._fx_gemm_wgrad = True  # gradient from the wgrad GEMM (fused-norm partials)
+        self.weight._fx_grad_chunked = self.sequence_parallel  # (as the column layer)
         if bias:
             self.bias = nn.Parameter(init_full_then_slice((out_features,), 0.0, name + ".bias",
                                                           dtype=dtype, device=device,

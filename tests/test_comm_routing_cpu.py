@@ -110,3 +110,27 @@ def test_stream_inventory_counts_peer_waiting_streams():
     assert names[0] == "compute"
     assert sum(1 for n in names if n.startswith("rccl:")) == 2
     assert all(p for n, p in inv if n.startswith("rccl:"))
+
+
+def _world_flag_worker(rank, world):
+    # ranks with and without communicators (as pipeline stages have) must
+    # agree on whether the world MAX of the one-shot error flag runs
+    from types import SimpleNamespace as NS
+    from fleetx_amd.parallel import comm
+    import os
+    comm._COMMS.clear()
+    if rank == 0:
+        comm._COMMS[(0, 1)] = NS(tried_oneshot=True, oneshot=None)
+    res = [comm.world_oneshot_possible()]
+    os.environ["FLEETX_ONESHOT_FORCE"] = "1"
+    torch.cuda.is_available = lambda: True  # what the GPU box reports
+    res.append(comm.world_oneshot_possible())
+    os.environ["FLEETX_ONESHOT"] = "0"
+    res.append(comm.world_oneshot_possible())
+    comm._COMMS.clear()
+    return res
+
+
+def test_world_error_flag_decision_is_rank_invariant():
+    res = dist_utils.run(_world_flag_worker, 2)
+    assert res[0] == res[1] == [False, True, False], res

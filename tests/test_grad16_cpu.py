@@ -123,3 +123,21 @@ def test_grad16_data_parallel_reduction():
     for n in a[0]:
         assert torch.equal(a[0][n], a[1][n]), n          # every rank holds the same mean
         assert torch.allclose(a[0][n], b[0][n], rtol=2e-2, atol=1e-5), n
+
+
+def test_sequence_parallel_weights_keep_fp32_gradients():
+    """The SP-overlapped backward writes a weight's gradient chunk by chunk
+    (``parallel/sp_overlap.py _wgrad_chunks``): 16-bit storage would round it
+    once per chunk, so those weights are not eligible."""
+    from fleetx_amd.parallel import layers as L
+    from fleetx_amd.parallel import topology as topo
+    old = topo.mp_world_size
+    try:
+        topo.mp_world_size = lambda: 2  # construction only reads the TP degree
+        col = L.ColumnParallelLinear(32, 64, sequence_parallel=True, dtype=torch.bfloat16)
+        row = L.RowParallelLinear(64, 32, sequence_parallel=True, dtype=torch.bfloat16)
+        plain = L.ColumnParallelLinear(32, 64, sequence_parallel=False, dtype=torch.bfloat16)
+    finally:
+        topo.mp_world_size = old
+    assert not grad16_eligible(col.weight) and not grad16_eligible(row.weight)
+    assert grad16_eligible(plain.weight)

@@ -78,7 +78,10 @@ def _train_gpu(rank, world, layout, steps=3, extra=()):
         gnorms.append(float(eng.optimizer.last_grad_norm))
     torch.cuda.synchronize()
     from fleetx_amd.ops import _lib
+    eng.optimizer.sync_state()
+    pf = eng.optimizer.buffer.param_flat
     return {"losses": losses, "gnorms": gnorms, "pnorm": _master_norm(eng), "drank": drank,
+            "pflat": pf.detach().float().cpu(),
             "native": _lib.kernels() is not None, "master": gather_master_state(eng),
             "master0": master0,
             "overlap": getattr(eng.optimizer, "_overlap_groups", None) is not None}
@@ -221,10 +224,19 @@ def _train_gpu_oneshot(rank, world, layout):
     return res
 
 
-@pytest.mark.parametrize("name", ["tp2", "tp2_sp"])
+@pytest.mark.parametrize("name", ["tp2", "tp2_sp", "pp2_tp2", "pp2_tp2_sp"])
 def test_tp_oneshot_allreduce_matches_single_rank(ref_gpu, name):
-    out = dist_utils.run(_train_gpu_oneshot, 2, LAYOUTS[name], timeout=300)
-    assert all(r["oneshot_calls"] > 0 for r in out), [r["oneshot_calls"] for r in out]
+    """With PP x TP the stages reach different collectives (the first stage
+    never calls the CE all-reduce, middle stages only the overlapped TP
+    paths), so their lazily created communicators differ: the world MAX of
+    the one-shot error flag must still run on every rank each step
+    (``comm.world_oneshot_possible``), or the ranks that skip it hang the
+    ones that enter it."""
+    layout = dict(LAYOUTS, pp2_tp2=(1, 2, 2, 1, 0, 2, False, 1),
+                  pp2_tp2_sp=(1, 2, 2, 1, 0, 2, True, 1))[name]
+    world = layout[0] * layout[1] * layout[2] * layout[3]
+    out = dist_utils.run(_train_gpu_oneshot, world, layout, timeout=300)
+    assert any(r["oneshot_calls"] > 0 for r in out), [r["oneshot_calls"] for r in out]
     _check(out, ref_gpu)
 
 
@@ -268,3 +280,23 @@ def test_overlapped_update_is_bitwise_serial(name):
         assert set(ra["master"]) == set(rb["master"])
         for k in ra["master"]:
             assert torch.equal(ra["master"][k], rb["master"][k]), k
+
+
+def _train_gpu_opt(rank, world, layout, name):
+    return _train_gpu(rank, world, layout, extra=("Optimizer.name=%s" % name,))
+
+
+@pytest.mark.parametrize("opt", ["Adam", "Momentum"])
+def test_zero1_other_optimizers_gather_params(opt):
+    """ZeRO-1 with Adam (L2 decay) and Momentum: every rank's replicated
+    bf16 parameters must be the same after each update (the overlapped
+    update issues the per-bucket gathers only for the AdamW family that has
+    it; the others gather in step()), and the run must match one rank."""
+    ref = dist_utils.run(_train_gpu_opt, 1, (1, 1, 1, 1, 0, GBS, False, 1), opt, timeout=300)[0]
+    out = dist_utils.run(_train_gpu_opt, 2, LAYOUTS["zero1"], opt, timeout=300)
+    assert torch.equal(out[0]["pflat"], out[1]["pflat"])
+    got = [(a + b) / 2 for a, b in zip(out[0]["losses"], out[1]["losses"])]
+    for a, b in zip(got, ref["losses"]):
+        assert abs(a - b) < 1.5e-2 * abs(b), (got, ref["losses"])
+    d = float((out[0]["pflat"] - ref["pflat"]).norm()) / float(ref["pflat"].norm())
+    assert d < 2e-2, d
