@@ -9,7 +9,7 @@ for v in $VARIANTS; do
   tag=${v%%:*}
   envs=${v#*:}
   env ${envs//,/ } FX_GEN_OUT=gen/g5v_$tag.inc python ../gen_gemm_asm.py
-  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -DFX_GEMM5_INC="\"$(pwd)/gen/g5v_$tag.inc\"" \
+  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -I../../csrc/kernels -DFX_GEMM5_INC="\"$(pwd)/gen/g5v_$tag.inc\"" \
     -o bin/g5v_$tag gemm_lab.cpp gemm_legacy.hip ../../csrc/kernels/gemm5.hip &
 done
 wait

@@ -75,6 +75,19 @@ int main(int argc, char** argv) {
       CK(hipEventSynchronize(e1));
       float ms; CK(hipEventElapsedTime(&ms, e0, e1));
       printf(", \"%s\": %.1f", c.nm, fl / (ms / iters * 1e-3) / 1e12);
+      if (getenv("LAB_HASH")) {
+        // output checksum of one launch into a zeroed C: schedule variants of
+        // the same kernel accumulate in the same order, so equal hashes
+        const size_t bytes = (size_t)c.m * c.ldc * (c.epi == 3 ? 4 : 2);
+        CK(hipMemset(c.C, 0, bytes));
+        run();
+        CK(hipDeviceSynchronize());
+        std::vector<unsigned char> hb(bytes);
+        CK(hipMemcpy(hb.data(), c.C, bytes, hipMemcpyDeviceToHost));
+        unsigned long long hsh = 1469598103934665603ull;
+        for (size_t i = 0; i < bytes; ++i) hsh = (hsh ^ hb[i]) * 1099511628211ull;
+        printf(", \"%s_h\": \"%016llx\"", c.nm, hsh);
+      }
       if (stamp_case) {
         char want[64];
         snprintf(want, sizeof(want), "%s:%s", s.name, c.nm);

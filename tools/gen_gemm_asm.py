@@ -140,13 +140,15 @@ def mfma(dt, st, s, i, j):
                                        vreg(FRAG("A", s) + 4 * i, 4), k))
 
 
-def segment(dt, st, s, rows, extras, read_gap, dma_gap, close=None):
-    """MFMAs of k-step s for fragment rows `rows` (x nf columns) with `extras`
-    (list of ('read', [(key, text)...]) / ('dma', (setup, groups))) interleaved:
-    reads one per `read_gap` MFMAs from the start, DMA loads one per `dma_gap`
-    MFMAs.  `close` = wait line ('lgkm0' = drain the scoreboard) emitted before
-    the last MFMA, followed by s_barrier after it."""
-    mf = [(s, i, j) for i in rows for j in range(GEO["nf"])]
+def segment(dt, st, s, rows, extras, read_gap, dma_gap, close=None, mf=None):
+    """MFMAs of k-step s for fragment rows `rows` (x nf columns) -- or the
+    explicit (s, i, j) list `mf` -- with `extras` (list of ('read', [(key,
+    text)...]) / ('dma', (setup, groups))) interleaved: reads one per
+    `read_gap` MFMAs from the start, DMA loads one per `dma_gap` MFMAs.
+    `close` = wait line ('lgkm0' = drain the scoreboard) emitted before the
+    last MFMA, followed by s_barrier after it."""
+    if mf is None:
+        mf = [(s, i, j) for i in rows for j in range(GEO["nf"])]
     reads = [x for kind, xs in extras if kind == "read" for x in xs]
     setup, groups = [], []
     for kind, xs in extras:
@@ -248,6 +250,65 @@ def generate(la, lb, dt, read_gap=1, dma_gap=3):
 
 
 def body_with(st, la, lb, dt, kind, read_gap, dma_gap):
+    if CFG.get("sched") == "2bar":
+        return body_2bar(st, la, lb, dt, kind, read_gap, dma_gap)
+    return body_4bar(st, la, lb, dt, kind, read_gap, dma_gap)
+
+
+def body_2bar(st, la, lb, dt, kind, read_gap, dma_gap):
+    """One K-tile iteration with TWO barriers (FX_GEN_SCHED=2bar):
+      P1  k0 rows 0..p1-1        + every k1 fragment read (A then B)
+          -> lgkm0, barrier: the whole buffer of tile t is in registers
+      P2  k0 rows p1..nf-1, k1 rows 0..nf-p3-1 + B(t+2) then A(t+2) DMA
+          -> vmcnt(2 nf): tile t+1 landed, barrier
+      P3  k1 rows nf-p3..nf-1    + tile t+1's k0 reads (B then A)
+    The k0 and k1 fragment sets of tile t are both live during P1/P2 (the
+    same 4 x 4 nf registers as the 4-barrier body)."""
+    lay = {"A": la, "B": lb}
+
+    def reads(op, s, which, idxs):
+        return [r for i in idxs for r in read_ops(lay[op], op, s, i, which)]
+
+    full, last = kind == "full", kind == "last"
+    nf, X = GEO["nf"], "0x%x" % GEO["buf"]
+    p1 = CFG.get("p1", (5 * nf) // 8)
+    mc = lay["A"] == MC or lay["B"] == MC
+    p3 = CFG.get("p3", nf // 2 if mc else (3 * nf) // 8)
+    allmf = [(0, i, j) for i in range(nf) for j in range(nf)] + \
+            [(1, i, j) for i in range(nf) for j in range(nf)]
+    n1, n3 = p1 * nf, p3 * nf
+    mf1, mf2, mf3 = allmf[:n1], allmf[n1:len(allmf) - n3], allmf[len(allmf) - n3:]
+    segment(dt, st, 0, None, [("read", reads("A", 1, "cur", range(nf)) +
+                                reads("B", 1, "cur", range(nf)))],
+            read_gap, dma_gap, close=None if last else "lgkm0", mf=mf1)
+    ex = []
+    if full:
+        sB, gB = dma_ops("B")
+        sA, gA = dma_ops("A")
+        ex.append(("dma", (sB, gB + [sA + gA[0]] + gA[1:])))
+    if last:
+        segment(dt, st, 0, None, ex, read_gap, dma_gap, mf=mf2 + mf3)
+        st.emit("s_nop 15")
+        st.emit("s_nop 15")
+        return st.lines, st.pending
+    segment(dt, st, 0, None, ex, read_gap, dma_gap,
+            close="s_waitcnt vmcnt(%d)" % (2 * nf if full else 0), mf=mf2)
+    segment(dt, st, 0, None, [("read", reads("B", 0, "nxt", range(nf)) +
+                                reads("A", 0, "nxt", range(nf)))], 1, dma_gap, mf=mf3)
+    for op in "AB":
+        if lay[op] == KC:
+            st.emit("v_xor_b32 %%[r%s_cur], %s, %%[r%s_cur]" % (op, X, op))
+            st.emit("v_xor_b32 %%[r%s_nxt], %s, %%[r%s_nxt]" % (op, X, op))
+        else:
+            for w in ("curlo", "curhi", "nxtlo", "nxthi"):
+                st.emit("v_xor_b32 %%[r%s_%s], %s, %%[r%s_%s]" % (op, w, X, op, w))
+        st.emit("s_xor_b32 %%[m%s], %%[m%s], %s" % (op, op, X))
+        if full:
+            st.emit("s_add_u32 %%[so%s], %%[so%s], %%[ks%s]" % (op, op, op))
+    return st.lines, st.pending
+
+
+def body_4bar(st, la, lb, dt, kind, read_gap, dma_gap):
     """One K-tile iteration.  kind: 'full' (stages t+2, reads t+1),
     'nodma' (reads t+1, stages nothing), 'last' (neither)."""
     lay = {"A": la, "B": lb}
@@ -341,13 +402,21 @@ def main():
                       int(os.environ.get("FX_GEN_STAGGER", "1"))),
              "T128": (int(os.environ.get("FX_GEN_DMA_GAP_T128", "2")), 0)}
     CFG["dma_start"] = int(os.environ.get("FX_GEN_DMA_START", "0"))
+    # K-loop structure per geometry: "4bar" (default) or "2bar" (body_2bar)
+    scheds = {"T256": os.environ.get("FX_GEN_SCHED_T256", os.environ.get("FX_GEN_SCHED", "4bar")),
+              "T128": os.environ.get("FX_GEN_SCHED_T128", os.environ.get("FX_GEN_SCHED", "4bar"))}
+    for key, env in (("p1", "FX_GEN_P1"), ("p3", "FX_GEN_P3")):
+        if os.environ.get(env):
+            CFG[key] = int(os.environ[env])
     parts = ["// GENERATED by tools/gen_gemm_asm.py -- do not edit.\n"
              "// K-loops of gemm5_kernel (csrc/kernels/gemm5.hip); read_gap=%d, "
-             "(dma_gap, stagger) T256=%s T128=%s\n" % (read_gap, knobs["T256"], knobs["T128"])]
+             "(dma_gap, stagger) T256=%s T128=%s, sched %s\n" % (read_gap, knobs["T256"],
+                                                                 knobs["T128"], scheds)]
     names = {KC: "KC", MC: "MC"}
     for tag in ("T256", "T128"):
         set_geometry(tag)
         dma_gap, CFG["stagger"] = knobs[tag]
+        CFG["sched"] = scheds[tag]
         for la, lb in ((KC, KC), (KC, MC), (MC, MC)):
             for dt in ("bf16", "f16"):
                 lines = ablate(generate(la, lb, dt, read_gap, dma_gap))
