@@ -821,212 +821,6 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_kernel(AttnParams P) {
   }
 }
 
-// ============================================================================
-// backward dQ, one wave per SIMD: WG = 4 waves x 64 queries = 256 queries.
-// Each wave owns two 32-query blocks, so every K / V fragment read from LDS
-// (row form for S^T and dP^T, transposed K for dQ) feeds two MFMAs.  Q and dO
-// of both blocks stay in registers (128), the dQ accumulators take 128 more:
-// one workgroup per CU.  Same element math and dropout hash as
-// fa_bwd_dq_kernel (bitwise-equal dQ and delta).
-// ============================================================================
-template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
-__global__ __launch_bounds__(256, 1) void fa_bwd_dq64_kernel(AttnParams P) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NW = 4, KV = 64, TB = KV * D * 2, QB = 64 * NW;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-  Frag<D> F;
-  F.init(lane);
-  const int nq = (P.Sq + QB - 1) / QB;
-  const int nblk = nq * P.B * P.H;
-  const int lid = xcd_remap(blockIdx.x, nblk);
-  int bh, qblock;
-  if constexpr (CAUSAL) {
-    int rank;
-    lpt_order(lid, nq, P.B * P.H, bh, rank);
-    qblock = nq - 1 - rank;
-  } else {
-    bh = lid / nq;
-    qblock = lid % nq;
-  }
-  const int b = bh / P.H, hd = bh % P.H;
-  const uint16_t* qp = P.q + b * P.sq_b + hd * P.sq_h;
-  const uint16_t* kp = P.k + b * P.sk_b + hd * P.sk_h;
-  const uint16_t* vp = P.v + b * P.sv_b + hd * P.sv_h;
-  const uint16_t* dop = P.dout + b * P.so_b + hd * P.so_h;
-  int kv_len = P.Sk;
-  if (P.kv_lens) kv_len = min(kv_len, P.kv_lens[b]);
-
-  const int wq0 = qblock * QB + w * 64;
-  int qi[2];
-  float lse2[2], dlt[2];
-  short8 qf[2][D / 16], gf[2][D / 16];
-#pragma unroll
-  for (int a = 0; a < 2; ++a) {
-    qi[a] = wq0 + 32 * a + (lane & 31);
-    const bool qvalid = qi[a] < P.Sq;
-#pragma unroll
-    for (int s = 0; s < D / 16; ++s) {
-      if (qvalid && 16 * s + 8 * h < P.dval) {
-        qf[a][s] = *reinterpret_cast<const short8*>(qp + (long)qi[a] * P.sq_s + 16 * s + 8 * h);
-        gf[a][s] = *reinterpret_cast<const short8*>(dop + (long)qi[a] * P.so_s + 16 * s + 8 * h);
-      } else {
-        qf[a][s] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
-        gf[a][s] = qf[a][s];
-      }
-    }
-    lse2[a] = qvalid ? P.lse[(long)bh * P.Sq + qi[a]] * LOG2E : INFINITY;
-  }
-  const float sl2 = P.scale * LOG2E;
-  const uint32_t cb = DROP ? attn_cb(P, bh) : 0u;
-
-  int kv_end = kv_len;
-  if (CAUSAL) kv_end = min(kv_end, (qblock + 1) * QB);
-  const int ntiles = (kv_end + KV - 1) / KV;
-
-  floatx16 dqacc[2][D / 32];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) dqacc[a][dt][i] = 0.f;
-
-  GldsStream<D, KV, NW> kld, vld;
-  kld.init(kp, P.sk_s, kv_end, w, lane, P.dval);
-  vld.init(vp, P.sv_s, kv_end, w, lane, P.dval);
-  if (ntiles > 0) {
-    kld.load(0, smem, lane);
-    vld.load(0, smem + 2 * TB, lane);
-  }
-#pragma unroll
-  for (int a = 0; a < 2; ++a) {
-    const bool qvalid = qi[a] < P.Sq;
-    float part = 0.f;
-    if (qvalid) {
-      const uint16_t* orow = P.o + b * P.so_b + hd * P.so_h + (long)qi[a] * P.so_s;
-#pragma unroll
-      for (int s = 0; s < D / 16; ++s) {
-        if (16 * s + 8 * h >= P.dval) continue;
-        float ov[8], gv[8];
-        load8<T>(orow + 16 * s + 8 * h, ov);
-        unpack8<T>(__builtin_bit_cast(uint4, gf[a][s]), gv);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) part += ov[j] * gv[j];
-      }
-    }
-    part += __shfl_xor(part, 32, 64);
-    dlt[a] = qvalid ? part : 0.f;
-    if (qvalid && h == 0) P.delta[(long)bh * P.Sq + qi[a]] = dlt[a];
-  }
-  glds_wait();
-  __syncthreads();
-
-  for (int it = 0; it < ntiles; ++it) {
-    const int cur = it & 1;
-    const char* kt = smem + cur * TB;
-    const char* vt = smem + 2 * TB + cur * TB;
-    const bool more = it + 1 < ntiles;
-    if (more) {
-      kld.load((it + 1) * KV, smem + (cur ^ 1) * TB, lane);
-      vld.load((it + 1) * KV, smem + 2 * TB + (cur ^ 1) * TB, lane);
-    }
-    const int kb = it * KV;
-    if (wq0 < P.Sq && !(CAUSAL && kb > wq0 + 63)) {
-      const bool need_mask = (CAUSAL && kb + KV - 1 > wq0) || (kb + KV > kv_len);
-      const bool half2 = (kb + 32 < kv_len && !(CAUSAL && kb + 32 > wq0 + 63));
-#pragma unroll 1
-      for (int t = 0; t < 2; ++t) {
-        if (t == 1 && !half2) continue;
-        floatx16 sacc[2], dpacc[2];
-        short8 dfs[2][2];
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) sacc[a][i] = dpacc[a][i] = 0.f;
-        short8 kr = F.row(kt, t, 0), vr = F.row(vt, t, 0);
-#pragma unroll
-        for (int s = 0; s < D / 16; ++s) {
-          asm volatile("" ::: "memory");
-          short8 nk = kr, nv = vr;
-          if (s + 1 < D / 16) {
-            nk = F.row(kt, t, s + 1);
-            nv = F.row(vt, t, s + 1);
-          }
-          sacc[0] = mfma<T>(kr, qf[0][s], sacc[0]);
-          sacc[1] = mfma<T>(kr, qf[1][s], sacc[1]);
-          dpacc[0] = mfma<T>(vr, gf[0][s], dpacc[0]);
-          dpacc[1] = mfma<T>(vr, gf[1][s], dpacc[1]);
-          kr = nk; vr = nv;
-        }
-#pragma unroll
-        for (int a = 0; a < 2; ++a) {
-          if constexpr (KB)
-            key_bias_add1(sacc[a], P.kbias + (long)b * P.kb_b + kb + 32 * t, h, sl2);
-          if (__builtin_expect(need_mask, 0)) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              const int key = kb + 32 * t + crow(i, h);
-              if ((CAUSAL && key > qi[a]) || key >= kv_len) sacc[a][i] = -INFINITY;
-            }
-          }
-          const float sc = KB ? 1.f : sl2;
-          // dS straight to 16-bit: the fp32 S / dP tiles die here
-#pragma unroll
-          for (int i = 0; i < 16; i += 2) {
-            const float p0 = fexp2(__builtin_fmaf(sacc[a][i], sc, -lse2[a]));
-            const float p1 = fexp2(__builtin_fmaf(sacc[a][i + 1], sc, -lse2[a]));
-            float dp0 = dpacc[a][i], dp1 = dpacc[a][i + 1];
-            float d0, d1;
-            if (DROP) {
-              const int key = kb + 32 * t + crow(i, h);
-              const uint32_t hh = lowbias32((((uint32_t)qi[a]) << 16 | ((uint32_t)key >> 1)) ^ cb);
-              dp0 = ((hh & 0xffffu) >= P.thr) ? dp0 : 0.f;
-              dp1 = ((hh >> 16) >= P.thr) ? dp1 : 0.f;
-              d0 = p0 * __builtin_fmaf(dp0, P.drop_scale, -dlt[a]);
-              d1 = p1 * __builtin_fmaf(dp1, P.drop_scale, -dlt[a]);
-            } else {
-              d0 = p0 * (dp0 - dlt[a]);
-              d1 = p1 * (dp1 - dlt[a]);
-            }
-            dfs[a][i >> 3][i & 7] = cvt16<T>(d0);
-            dfs[a][i >> 3][(i & 7) + 1] = cvt16<T>(d1);
-          }
-        }
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          v4s klo[D / 32], khi[D / 32];
-          F.tr_issue(kt, t, ss, klo, khi);
-          tr_wait(klo, khi);
-#pragma unroll
-          for (int dt = 0; dt < D / 32; ++dt) {
-            const short8 k8 = tr_join(klo[dt], khi[dt]);
-            dqacc[0][dt] = mfma<T>(k8, dfs[0][ss], dqacc[0][dt]);
-            dqacc[1][dt] = mfma<T>(k8, dfs[1][ss], dqacc[1][dt]);
-          }
-        }
-      }
-    }
-    glds_wait();
-    __syncthreads();
-  }
-#pragma unroll
-  for (int a = 0; a < 2; ++a) {
-    if (qi[a] >= P.Sq) continue;
-    uint16_t* dqp = P.dq + b * P.sdq_b + hd * P.sdq_h + (long)qi[a] * P.sdq_s;
-#pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        ushort4 o;
-        o.x = Elt<T>::from_f(dqacc[a][dt][4 * g + 0] * P.scale);
-        o.y = Elt<T>::from_f(dqacc[a][dt][4 * g + 1] * P.scale);
-        o.z = Elt<T>::from_f(dqacc[a][dt][4 * g + 2] * P.scale);
-        o.w = Elt<T>::from_f(dqacc[a][dt][4 * g + 3] * P.scale);
-        if (dt * 32 + 8 * g + 4 * h < P.dval)
-          *reinterpret_cast<ushort4*>(dqp + dt * 32 + 8 * g + 4 * h) = o;
-      }
-  }
-}
 
 // swap a 32-bit value with the neighbouring lane (lane ^ 1) through DPP
 __device__ __forceinline__ uint32_t dpp_swap1(uint32_t v) {
@@ -1313,249 +1107,10 @@ __device__ __forceinline__ void dkdv_body(const AttnParams& P, char* smem) {
   }
 }
 
-// ============================================================================
-// backward dK/dV, one wave per SIMD: WG = 4 waves x 64 keys = 256 keys.
-// Each wave owns two 32-key blocks, so every Q / dO fragment read from LDS
-// (row form for S and dP, transposed form for dK and dV) feeds two MFMAs
-// instead of one.  That is 40 % less LDS traffic per FLOP than dkdv_body,
-// which is LDS-bound at two waves per SIMD.  The dK / dV accumulators of both
-// blocks (256 registers) and the K fragments (64) need the whole 512-register
-// file, so one workgroup runs per CU and V is read from an LDS image of the
-// workgroup's 256 rows.  Same element math and dropout hash as dkdv_body
-// (bitwise-equal results).
-// ============================================================================
-template <typename T, int D, bool CAUSAL, bool DROP, bool KB, int QT>
-__device__ __forceinline__ void dkdv64_body(const AttnParams& P, char* smem) {
-  constexpr int NW = 4;
-  constexpr int KR = 64 * NW;  // keys per workgroup
-  constexpr int TB = QT * D * 2;
-  constexpr int BUF = 2 * TB + 2 * QT * 4;
-  char* vs = smem + 2 * BUF;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-  Frag<D> F;
-  F.init(lane);
-  const int nk = (P.Sk + KR - 1) / KR;
-  const int nblk = nk * P.B * P.H;
-  const int lid = xcd_remap(blockIdx.x, nblk);
-  int bh, kblock;
-  if constexpr (CAUSAL) {
-    lpt_order(lid, nk, P.B * P.H, bh, kblock);
-  } else {
-    bh = lid / nk;
-    kblock = lid % nk;
-  }
-  const int b = bh / P.H, hd = bh % P.H;
-  const uint16_t* qp = P.q + b * P.sq_b + hd * P.sq_h;
-  const uint16_t* kp = P.k + b * P.sk_b + hd * P.sk_h;
-  const uint16_t* vp = P.v + b * P.sv_b + hd * P.sv_h;
-  const uint16_t* dop = P.dout + b * P.so_b + hd * P.so_h;
-  int kv_len = P.Sk;
-  if (P.kv_lens) kv_len = min(kv_len, P.kv_lens[b]);
+#ifdef FX_FA_LAB
+#include FX_FA_LAB  // tools/fa_lab/fa_wave64.inc (lab builds only)
+#endif
 
-  const int wk0 = kblock * KR + w * 64;
-  int ki[2];
-  float kb2[2];
-  short8 kf[2][D / 16];
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb) {
-    ki[kb] = wk0 + 32 * kb + (lane & 31);
-    kb2[kb] = ki[kb] >= kv_len ? -INFINITY
-                               : (KB ? P.kbias[(long)b * P.kb_b + ki[kb]] * LOG2E : 0.f);
-#pragma unroll
-    for (int s = 0; s < D / 16; ++s) {
-      if (ki[kb] < P.Sk && 16 * s + 8 * h < P.dval)
-        kf[kb][s] = *reinterpret_cast<const short8*>(kp + (long)ki[kb] * P.sk_s + 16 * s + 8 * h);
-      else
-        kf[kb][s] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
-    }
-  }
-  Glds<D, KR, NW>::load(vp, P.sv_s, kblock * KR, P.Sk, vs, w, lane, P.dval);
-  floatx16 dkacc[2][D / 32], dvacc[2][D / 32];
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) dkacc[kb][dt][i] = dvacc[kb][dt][i] = 0.f;
-  const float sl2 = P.scale * LOG2E;
-  const uint32_t cb = DROP ? attn_cb(P, bh) : 0u;
-
-  const int q_begin = CAUSAL ? (kblock * KR / QT) * QT : 0;
-  const int ntiles = P.Sq > q_begin ? (P.Sq - q_begin + QT - 1) / QT : 0;
-  float nl = INFINITY, nd = 0.f;
-  auto rowconst_load = [&](int qb) {
-    if (tid < QT) {
-      const int q = qb + tid;
-      nl = q < P.Sq ? P.lse[(long)bh * P.Sq + q] * LOG2E : INFINITY;
-      nd = q < P.Sq ? P.delta[(long)bh * P.Sq + q] : 0.f;
-    }
-  };
-  auto rowconst_store = [&](char* buf) {
-    if (tid < QT) {
-      float* c = reinterpret_cast<float*>(buf + 2 * TB);
-      c[tid] = nl;
-      c[QT + tid] = nd;
-    }
-  };
-  GldsStream<D, QT, NW> qld, gld;
-  qld.init(qp, P.sq_s, P.Sq, w, lane, P.dval);
-  gld.init(dop, P.so_s, P.Sq, w, lane, P.dval);
-  if (ntiles > 0) {
-    rowconst_load(q_begin);
-    qld.load(q_begin, smem, lane);
-    gld.load(q_begin, smem + TB, lane);
-    rowconst_store(smem);
-  }
-  glds_wait();
-  __syncthreads();
-
-  for (int it = 0; it < ntiles; ++it) {
-    const int qb = q_begin + it * QT;
-    const char* cur = smem + (it & 1) * BUF;
-    char* nxt = smem + ((it & 1) ^ 1) * BUF;
-    const bool more = it + 1 < ntiles;
-    if (more) {
-      rowconst_load(qb + QT);
-      qld.load(qb + QT, nxt, lane);
-      gld.load(qb + QT, nxt + TB, lane);
-    }
-    const char* qt = cur;
-    const char* gt = cur + TB;
-    const float* lse_s = reinterpret_cast<const float*>(cur + 2 * TB);
-    const float* dl_s = lse_s + QT;
-    if (wk0 < P.Sk && !(CAUSAL && qb + QT - 1 < wk0)) {
-#pragma unroll 1
-      for (int t = 0; t < QT / 32; ++t) {
-        const int q0 = qb + 32 * t;
-        if (CAUSAL && q0 + 31 < wk0) continue;
-        uint32_t keep[2] = {0u, 0u};
-        if (DROP) {
-#pragma unroll
-          for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int i = 0; i < 16; i += 2) {
-              const int q = q0 + crow(i, h);
-              const uint32_t mine =
-                  lowbias32((((uint32_t)(q + (lane & 1))) << 16 | ((uint32_t)ki[kb] >> 1)) ^ cb);
-              const uint32_t other = dpp_swap1(mine);
-              const uint32_t hq = (lane & 1) ? other : mine;
-              const uint32_t hq1 = (lane & 1) ? mine : other;
-              const uint32_t r0 = (lane & 1) ? (hq >> 16) : (hq & 0xffffu);
-              const uint32_t r1 = (lane & 1) ? (hq1 >> 16) : (hq1 & 0xffffu);
-              keep[kb] |= (r0 >= P.thr ? 1u : 0u) << i;
-              keep[kb] |= (r1 >= P.thr ? 1u : 0u) << (i + 1);
-            }
-        }
-        floatx16 sacc[2], dpacc[2];
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) sacc[kb][i] = dpacc[kb][i] = 0.f;
-        if (CAUSAL && __builtin_expect(q0 < wk0 + 63, 0)) {
-#pragma unroll
-          for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-              if (ki[kb] > q0 + crow(i, h)) sacc[kb][i] = -INFINITY;
-        }
-        // fragments one k-step ahead, no further: the compiler would otherwise
-        // hoist every k-step's LDS reads to the top (64+ registers) and spill
-        short8 qr = F.row(qt, t, 0), gr = F.row(gt, t, 0);
-        short8 v0 = F.row(vs, 2 * w, 0), v1 = F.row(vs, 2 * w + 1, 0);
-#pragma unroll
-        for (int s = 0; s < D / 16; ++s) {
-          asm volatile("" ::: "memory");
-          short8 nq = qr, ng = gr, nv0 = v0, nv1 = v1;
-          if (s + 1 < D / 16) {
-            nq = F.row(qt, t, s + 1);
-            ng = F.row(gt, t, s + 1);
-            nv0 = F.row(vs, 2 * w, s + 1);
-            nv1 = F.row(vs, 2 * w + 1, s + 1);
-          }
-          sacc[0] = mfma<T>(qr, kf[0][s], sacc[0]);
-          sacc[1] = mfma<T>(qr, kf[1][s], sacc[1]);
-          dpacc[0] = mfma<T>(gr, v0, dpacc[0]);
-          dpacc[1] = mfma<T>(gr, v1, dpacc[1]);
-          qr = nq; gr = ng; v0 = nv0; v1 = nv1;
-        }
-        // P o Z and dS of both key blocks to 16-bit first: the fp32 S / dP
-        // tiles (64 registers) die before the fragment reads of the MFMA phase
-        short8 pf[2][2], df[2][2];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int ql_ = 32 * t + crow(i, h);
-          const float lse_q = lse_s[ql_], dl_q = dl_s[ql_];
-#pragma unroll
-          for (int kb = 0; kb < 2; ++kb) {
-            const float p = fexp2(__builtin_fmaf(sacc[kb][i], sl2, kb2[kb] - lse_q));
-            if (DROP) {
-              const float z = ((keep[kb] >> i) & 1u) ? P.drop_scale : 0.f;
-              pf[kb][i >> 3][i & 7] = cvt16<T>(p * z);
-              df[kb][i >> 3][i & 7] = cvt16<T>(p * (dpacc[kb][i] * z - dl_q));
-            } else {
-              pf[kb][i >> 3][i & 7] = cvt16<T>(p);
-              df[kb][i >> 3][i & 7] = cvt16<T>(p * (dpacc[kb][i] - dl_q));
-            }
-          }
-        }
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          v4s glo[D / 32], ghi[D / 32];
-          F.tr_issue(gt, t, ss, glo, ghi);
-          tr_wait(glo, ghi);
-#pragma unroll
-          for (int dt = 0; dt < D / 32; ++dt) {
-            const short8 g8 = tr_join(glo[dt], ghi[dt]);
-            dvacc[0][dt] = mfma<T>(g8, pf[0][ss], dvacc[0][dt]);
-            dvacc[1][dt] = mfma<T>(g8, pf[1][ss], dvacc[1][dt]);
-          }
-          v4s qlo[D / 32], qhi[D / 32];
-          F.tr_issue(qt, t, ss, qlo, qhi);
-          tr_wait(qlo, qhi);
-#pragma unroll
-          for (int dt = 0; dt < D / 32; ++dt) {
-            const short8 q8 = tr_join(qlo[dt], qhi[dt]);
-            dkacc[0][dt] = mfma<T>(q8, df[0][ss], dkacc[0][dt]);
-            dkacc[1][dt] = mfma<T>(q8, df[1][ss], dkacc[1][dt]);
-          }
-        }
-      }
-    }
-    if (more) rowconst_store(nxt);
-    glds_wait();
-    __syncthreads();
-  }
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb) {
-    if (ki[kb] >= P.Sk) continue;
-    uint16_t* dkp = P.dk + b * P.sdk_b + hd * P.sdk_h + (long)ki[kb] * P.sdk_s;
-    uint16_t* dvp = P.dv + b * P.sdk_b + hd * P.sdk_h + (long)ki[kb] * P.sdk_s;
-#pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        ushort4 a, c;
-        a.x = Elt<T>::from_f(dkacc[kb][dt][4 * g + 0] * P.scale);
-        a.y = Elt<T>::from_f(dkacc[kb][dt][4 * g + 1] * P.scale);
-        a.z = Elt<T>::from_f(dkacc[kb][dt][4 * g + 2] * P.scale);
-        a.w = Elt<T>::from_f(dkacc[kb][dt][4 * g + 3] * P.scale);
-        c.x = Elt<T>::from_f(dvacc[kb][dt][4 * g + 0]);
-        c.y = Elt<T>::from_f(dvacc[kb][dt][4 * g + 1]);
-        c.z = Elt<T>::from_f(dvacc[kb][dt][4 * g + 2]);
-        c.w = Elt<T>::from_f(dvacc[kb][dt][4 * g + 3]);
-        if (dt * 32 + 8 * g + 4 * h < P.dval) {
-          *reinterpret_cast<ushort4*>(dkp + dt * 32 + 8 * g + 4 * h) = a;
-          *reinterpret_cast<ushort4*>(dvp + dt * 32 + 8 * g + 4 * h) = c;
-        }
-      }
-  }
-}
-
-template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
-__global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_k64_kernel(AttnParams P) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  dkdv64_body<T, D, CAUSAL, DROP, KB, FA_DKDV64_QT>(P, smem);
-}
 
 template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(AttnParams P) {
@@ -1567,12 +1122,6 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dkdv_q64v_kernel(AttnParams
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // launched for D <= 96 only (D = 128 has no registers for V; it would spill)
   if constexpr (D <= 96) dkdv_body<T, D, CAUSAL, DROP, KB, 64, true, NW>(P, smem);
-}
-// D = 128 with V in registers (FLEETX_FA_DKDV_VREG: lean register plan)
-template <typename T, int D, bool CAUSAL, bool DROP, bool KB>
-__global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_v128_kernel(AttnParams P) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  if constexpr (D == 128) dkdv_body<T, D, CAUSAL, DROP, KB, FA_DKDV_V128_QT, true>(P, smem);
 }
 
 AttnParams make_params(const void* q, const void* k, const void* v, const long* qs,
@@ -1646,39 +1195,32 @@ static bool fa_pair_grid() {
   return on;
 }
 
-// The D = 128 dK/dV pass with 64 keys per wave (dkdv64_body): FLEETX_FA_DKDV64
-// or fx_fa_set_dkdv64 (1 on, 0 off; < 0 re-reads the environment)
-static int g_dkdv64 = -1;
-static bool dkdv64() {
-  if (g_dkdv64 < 0) {
-    const char* e = getenv("FLEETX_FA_DKDV64");
-    g_dkdv64 = e ? (atoi(e) != 0) : 0;
+#ifdef FX_FA_LAB
+// Lab variants (tools/fa_lab): FLEETX_FA_DKDV64 (dK/dV with 64 keys per wave),
+// FLEETX_FA_DKDV_VREG (D = 128 dK/dV with V in registers), FLEETX_FA_DQ64 (dQ
+// with 64 queries per wave), or the fx_fa_set_* switches (1 on, 0 off, < 0
+// re-reads the environment)
+static int g_dkdv64 = -1, g_dkdv_vreg = -1, g_dq64 = -1;
+static bool lab_flag(int& g, const char* name) {
+  if (g < 0) {
+    const char* e = getenv(name);
+    g = e ? (atoi(e) != 0) : 0;
   }
-  return g_dkdv64 != 0;
+  return g != 0;
 }
+static bool dkdv64() { return lab_flag(g_dkdv64, "FLEETX_FA_DKDV64"); }
+static bool dkdv_vreg() { return lab_flag(g_dkdv_vreg, "FLEETX_FA_DKDV_VREG"); }
+static bool dq64() { return lab_flag(g_dq64, "FLEETX_FA_DQ64"); }
+extern "C" int fx_fa_lab() { return 1; }
 extern "C" void fx_fa_set_dkdv64(int on) { g_dkdv64 = on < 0 ? -1 : (on != 0); }
-// The D = 128 dK/dV pass with V in registers (fa_bwd_dkdv_v128_kernel):
-// FLEETX_FA_DKDV_VREG or fx_fa_set_dkdv_vreg (same convention)
-static int g_dkdv_vreg = -1;
-static bool dkdv_vreg() {
-  if (g_dkdv_vreg < 0) {
-    const char* e = getenv("FLEETX_FA_DKDV_VREG");
-    g_dkdv_vreg = e ? (atoi(e) != 0) : 0;
-  }
-  return g_dkdv_vreg != 0;
-}
 extern "C" void fx_fa_set_dkdv_vreg(int on) { g_dkdv_vreg = on < 0 ? -1 : (on != 0); }
-// The D = 128 dQ pass with 64 queries per wave (fa_bwd_dq64_kernel): FLEETX_FA_DQ64
-// or fx_fa_set_dq64 (same convention)
-static int g_dq64 = -1;
-static bool dq64() {
-  if (g_dq64 < 0) {
-    const char* e = getenv("FLEETX_FA_DQ64");
-    g_dq64 = e ? (atoi(e) != 0) : 0;
-  }
-  return g_dq64 != 0;
-}
 extern "C" void fx_fa_set_dq64(int on) { g_dq64 = on < 0 ? -1 : (on != 0); }
+#else
+extern "C" int fx_fa_lab() { return 0; }  // production build: no lab variants
+extern "C" void fx_fa_set_dkdv64(int) {}
+extern "C" void fx_fa_set_dkdv_vreg(int) {}
+extern "C" void fx_fa_set_dq64(int) {}
+#endif
 
 static int fwd_waves() {
   static int nw = [] {
@@ -1798,9 +1340,11 @@ static int flash_bwd_t(const void* q, const void* k, const void* v, const void* 
     if (D == 96 && waves_for(Sq) == 3) {
       const int nq = (Sq + 95) / 96;
       FA_DISPATCH_NW(fa_bwd_dq_kernel, 96, 3, causal, drop, kb, nq * B * H, smem, st, P);
+#ifdef FX_FA_LAB
     } else if (D == 128 && dq64()) {
       FA_DISPATCH_D(fa_bwd_dq64_kernel, 128, causal, drop, kb, (Sq + 255) / 256 * B * H, smem,
                     st, P);
+#endif
     } else {
       const int nq = (Sq + 127) / 128;
       FA_DISPATCH(fa_bwd_dq_kernel, D, causal, drop, kb, nq * B * H, smem, st, P);
@@ -1819,6 +1363,7 @@ static int flash_bwd_t(const void* q, const void* k, const void* v, const void* 
       const size_t smem = 2 * (2 * 64 * D * 2 + 2 * 64 * 4);
       FA_DISPATCH(fa_bwd_dkdv_q64v_kernel, D, causal, p > 0.f, kbias != nullptr, nk * B * H,
                   smem, st, P);
+#ifdef FX_FA_LAB
     } else if (dkdv_vreg()) {
       // D = 128, V in registers: no V image in LDS
       const size_t smem = 2 * (2 * FA_DKDV_V128_QT * D * 2 + 2 * FA_DKDV_V128_QT * 4);
@@ -1829,6 +1374,7 @@ static int flash_bwd_t(const void* q, const void* k, const void* v, const void* 
       const size_t smem = 2 * (2 * FA_DKDV64_QT * D * 2 + 2 * FA_DKDV64_QT * 4) + 256 * D * 2;
       FA_DISPATCH_D(fa_bwd_dkdv_k64_kernel, 128, causal, p > 0.f, kbias != nullptr,
                     (Sk + 255) / 256 * B * H, smem, st, P);
+#endif
     } else {
       const size_t smem = 2 * (2 * FA_DKDV_QT * D * 2 + 2 * FA_DKDV_QT * 4) + 128 * D * 2;
       FA_DISPATCH(fa_bwd_dkdv_kernel, D, causal, p > 0.f, kbias != nullptr, nk * B * H, smem,

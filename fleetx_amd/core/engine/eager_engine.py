@@ -75,16 +75,19 @@ class DynamicLossScaler:
         self.decr_every = int(decr_every)
 
     def update(self, found_inf):
+        """In place on the three device tensors (no host sync, no rebinding):
+        the whole-step HIP graph captures this update and every replay must
+        advance the SAME scale the next replay's backward multiplies by."""
         inf = found_inf.reshape(()).bool()
         zero = torch.zeros_like(self.good)
-        self.good = torch.where(inf, zero, self.good + 1)
-        self.bad = torch.where(inf, self.bad + 1, zero)
-        grow = self.good >= self.incr_every
-        shrink = self.bad >= self.decr_every
-        self.scale = torch.where(shrink, self.scale * self.decr_ratio,
-                                 torch.where(grow, self.scale * self.incr_ratio, self.scale))
-        self.good = torch.where(grow, zero, self.good)
-        self.bad = torch.where(shrink, zero, self.bad)
+        good = torch.where(inf, zero, self.good + 1)
+        bad = torch.where(inf, self.bad + 1, zero)
+        grow = good >= self.incr_every
+        shrink = bad >= self.decr_every
+        self.scale.copy_(torch.where(shrink, self.scale * self.decr_ratio,
+                                     torch.where(grow, self.scale * self.incr_ratio, self.scale)))
+        self.good.copy_(torch.where(grow, zero, good))
+        self.bad.copy_(torch.where(shrink, zero, bad))
 
     def state_dict(self):
         return {"scale": self.scale.cpu(), "good": self.good.cpu(), "bad": self.bad.cpu()}
@@ -216,9 +219,14 @@ class EagerEngine(BasicEngine):
                 # one MI355X: -4.4 ms (profiles/r5_grad16/)
                 gd = str(comm.get("grad_dtype", "auto"))
                 if gd == "auto":
-                    gd = "bfloat16" if (self._dtype == torch.bfloat16
-                                        and self._accumulate_steps == 1 and not self._pipeline
-                                        and self._sharding_stage == 0) else "float32"
+                    # fp16 O2 too (reference GradStorage is fp16 there): the
+                    # epilogue's norm partials are then of the stored fp16
+                    # values, so a gradient that overflows 16 bits makes the
+                    # norm non-finite and the loss scaler skips the step
+                    g16 = {torch.bfloat16: "bfloat16", torch.float16: "float16"}.get(self._dtype)
+                    gd = g16 if (g16 is not None and self._accumulate_steps == 1
+                                 and not self._pipeline
+                                 and self._sharding_stage == 0) else "float32"
                 gdt = {"float32": torch.float32, "bfloat16": torch.bfloat16,
                        "float16": torch.float16}[gd]
                 if gdt != torch.float32 and self._accumulate_steps > 1:
@@ -337,8 +345,10 @@ class EagerEngine(BasicEngine):
 
     # ------------------------------------------------------------------ HIP graph
     def _graph_ok(self, comm):
-        """Whole-step capture needs a single-rank, non-pipelined bf16 step with
-        device-resident optimizer state (no host syncs, no loss scaler)."""
+        """Whole-step capture needs a single-rank, non-pipelined step with
+        device-resident optimizer state (no host syncs).  The fp16 dynamic
+        loss scaler qualifies: scale, counters and found-inf stay on the
+        device and are updated in place (DynamicLossScaler.update)."""
         why = None
         if not torch.cuda.is_available() or self.device.type != "cuda":
             why = "no GPU"
@@ -346,8 +356,8 @@ class EagerEngine(BasicEngine):
             why = "multi-rank runs keep eager collectives"
         elif self._pipeline:
             why = "pipeline schedules run eagerly"
-        elif self._use_pure_fp16 and self._dtype == torch.float16:
-            why = "the fp16 loss scaler steps on the host"
+        elif self.scaler is not None and not hasattr(self.optimizer, "_update_overlapped"):
+            why = "%s reads found-inf on the host" % type(self.optimizer).__name__
         elif getattr(self.optimizer, "offload", False):
             why = "offloaded optimizer state"
         if why is not None:
@@ -394,10 +404,14 @@ class EagerEngine(BasicEngine):
             l = self._module.training_step(mb)
             if self._accumulate_steps > 1:
                 l = l / self._accumulate_steps
-            self._module.backward(l)
+            self._module.backward(l * self.scaler.scale if self.scaler is not None else l)
             loss = l.detach() if loss is None else loss + l.detach()
         self.buffer.finish()
         self.optimizer.step()
+        if self.scaler is not None:
+            # device-side GradScaler step (in place: the captured graph advances
+            # the same scale / counters every replay)
+            self.scaler.update(self.optimizer.found_inf)
         self.optimizer.clear_grad()
         if defer:
             self._graph_lr_pending.copy_(self._graph_lr)

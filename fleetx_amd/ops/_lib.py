@@ -19,7 +19,15 @@ def kernels():
     if _K is not None:
         return _K
     try:
-        from .._C import _kernels as k  # noqa: WPS433
+        lab = os.environ.get("FLEETX_KERNELS_LIB")
+        if lab:
+            # a lab build of the same library (tools/fa_lab/build.py)
+            import importlib.util
+            spec = importlib.util.spec_from_file_location("_kernels", lab)
+            k = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(k)
+        else:
+            from .._C import _kernels as k  # noqa: WPS433
         _K = k
         return k
     except ImportError as e:  # pragma: no cover - exercised on broken installs

@@ -20,7 +20,7 @@ CFG = os.path.join(os.path.dirname(__file__), "..", "fleetx_amd", "configs", "nl
 B, S, V = 4, 256, 2048
 
 
-def _engine(dtype):
+def _engine(dtype, extra=()):
     from fleetx_amd.utils import config as C
     from fleetx_amd.utils import env
     from fleetx_amd.models import build_module
@@ -33,7 +33,7 @@ def _engine(dtype):
           "Global.device=gpu", "Global.local_batch_size=%d" % B, "Global.micro_batch_size=%d" % B,
           "Engine.mix_precision.use_pure_fp16=True", "Engine.mix_precision.dtype=%s" % dtype,
           "Engine.mix_precision.scale_loss=1024.0", "Engine.max_steps=100",
-          "Data.Train.dataset.name=SyntheticGPTDataset"]
+          "Data.Train.dataset.name=SyntheticGPTDataset"] + list(extra)
     cfg = C.get_config(CFG, overrides=ov, nranks=1)
     cfg.Optimizer.lr = {"name": "ConstantLR", "learning_rate": 1e-3}
     env.init_dist_env(cfg)
@@ -87,3 +87,58 @@ def test_fp16_overflow_skips_update_and_scaler_backs_off():
     assert int(opt.found_inf.item()) == 0
     assert int(opt.dev_step.item()) == step0 + 1
     assert not torch.equal(eng.buffer.param_flat, params0)
+
+
+def _fp16_run(graph, overlap, steps=9, inject=(3, 4)):
+    """fp16 O2 steps with the scaler growing every 2 good steps; at step
+    inject[0] the scale is set to 2^40 (fp16 gradients overflow: skip, and
+    with decr_every 1 the scale halves), at inject[1] back to 1024."""
+    from fleetx_amd.ops import _lib
+    _lib.kernels().set_dropout_salt(0)
+    _lib.kernels().set_adamw_lr_ptr(0)
+    eng = _engine("float16", extra=(
+        "Engine.cuda_graph=%s" % graph, "Engine.mix_precision.incr_every_n_steps=2",
+        "Engine.mix_precision.decr_every_n_nan_or_inf=1",
+        "Distributed.comm.overlap_optimizer=%s" % overlap))
+    assert eng._cuda_graph == graph
+    sc, opt = eng.scaler, eng.optimizer
+    losses, scales, infs = [], [], []
+    for s in range(steps):
+        if s == inject[0]:
+            sc.scale.fill_(2.0 ** 40)
+        elif s == inject[1]:
+            sc.scale.fill_(1024.0)
+        losses.append(float(eng._fit_impl(_batch(s))))
+        torch.cuda.synchronize()
+        scales.append(float(sc.scale))
+        infs.append(int(opt.found_inf.item()))
+    opt.sync_state()
+    torch.cuda.synchronize()
+    out = {"losses": losses, "scales": scales, "infs": infs,
+           "params": eng.buffer.param_flat.detach().clone(), "step": int(opt.dev_step.item()),
+           "graph": eng._graph is not None, "gdtype": eng.buffer.grad_dtype}
+    _lib.kernels().set_dropout_salt(0)
+    _lib.kernels().set_adamw_lr_ptr(0)
+    return out
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_fp16_graph_replay_bitwise_eager_across_overflow_and_growth(monkeypatch, overlap):
+    """The fp16 step captured in the whole-step HIP graph (loss scaler
+    updated in place on the device) replays the eager step bit for bit:
+    through scale growth, an overflowed (skipped) step with its back-off,
+    and the manual reset -- with the serial and with the deferred overlapped
+    update.  fp16 O2 stores the GEMM-written gradients in fp16 (grad_dtype
+    auto), whose overflow the epilogue's norm partials report."""
+    monkeypatch.setenv("FLEETX_DETERMINISTIC", "1")
+    e = _fp16_run(False, overlap)
+    g = _fp16_run(True, overlap)
+    assert g["graph"] and not e["graph"]
+    assert e["gdtype"] == torch.float16 and g["gdtype"] == torch.float16
+    assert e["infs"][3] == 1 and sum(e["infs"]) == 1, e["infs"]
+    assert e["scales"][3] == 2.0 ** 39                      # overflow: halved
+    assert any(b == 2 * a for a, b in zip(e["scales"][4:], e["scales"][5:])), e["scales"]
+    assert e["step"] == 9 - 1                                  # the skipped step
+    assert e["losses"] == g["losses"], (e["losses"], g["losses"])
+    assert e["scales"] == g["scales"] and e["infs"] == g["infs"]
+    assert torch.equal(e["params"], g["params"])

@@ -6,11 +6,23 @@ the same MFMA sequence per 32-row block as the pass it replaces, so dQ / dK /
 dV must agree bitwise.  ``vreg``: the 2-wave dK/dV pass with V in registers
 (``fa_bwd_dkdv_v128_kernel``, FLEETX_FA_DKDV_VREG).  Shapes cover a key tail (Sk not a multiple of the 256-key
 workgroup), causal + dropout, key lengths and fp16."""
+import os
+
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
+# lab-only kernels: run with the lab library, e.g.
+#   python tools/fa_lab/build.py && FLEETX_KERNELS_LIB=tools/fa_lab/_kernels*.so \
+#     python -m pytest tools/fa_lab/test_fa_wave64_lab.py
+
+
+@pytest.fixture(autouse=True)
+def _lab_library():
+    from fleetx_amd.ops import _lib
+    if not _lib.kernels().fa_lab():
+        pytest.skip("production kernel library: build tools/fa_lab (FLEETX_KERNELS_LIB)")
 
 
 def _rel(a, b):
