@@ -120,7 +120,9 @@ extern "C" int fx_gemm(int dt, int la, int lb, int epi, int M, int N, int K, con
   }
   if (M <= 0 || N <= 0 || K < 2 * BK || K % BK) return -1;
   if (sq != nullptr && !epi_wgrad(epi)) return -5;
-  if (epi == EPI_F32B && beta) return -6;  // 16-bit gradients are written, never accumulated
+  // 16-bit gradients accumulate (beta: micro-batches, pipeline schedules) in
+  // the plain order only: one fp32 add + one rounding per write
+  if (ctr && beta) return -6;
   if (N % 4 || (la == LAY_MC && M % 8) || (lb == LAY_MC && N % 8)) return -2;
   if (M < 8 || N < 8) return -2;
   const long a_span = la == LAY_KC ? (long)M * lda : (long)BK * lda + M;

@@ -212,26 +212,26 @@ class EagerEngine(BasicEngine):
                 # 16-bit gradient storage for the GEMM-written weight matrices
                 # (reference O2: GradStorage in the parameter dtype,
                 # tensor_fusion_helper.py:56,72-74): the weight-gradient GEMM
-                # rounds its fp32 tile once and the update reads 2 B instead
-                # of 4 per parameter.  "auto": bf16 models that write each
-                # gradient once per step (no micro-batch accumulation, no
-                # pipeline schedule, no ZeRO); fp32 otherwise.  6.7B step on
-                # one MI355X: -4.4 ms (profiles/r5_grad16/)
+                # rounds its fp32 tile once per write and the update reads 2 B
+                # instead of 4 per parameter; the data-parallel reduction then
+                # runs in 16 bits, averaged first (grad_buffer._launch).
+                # "auto": 16-bit models (bf16; fp16 O2, where the epilogue's
+                # norm partials are of the stored fp16 values so an overflow
+                # makes the norm non-finite and the scaler skips the step)
+                # without ZeRO sharding; micro-batch accumulation and pipeline
+                # schedules add each micro-batch into the 16-bit storage (one
+                # fp32 add + one rounding per write, as the reference's 16-bit
+                # GradStorage accumulates).  6.7B step on one MI355X: -4.4 ms
+                # (profiles/r5_grad16/)
                 gd = str(comm.get("grad_dtype", "auto"))
                 if gd == "auto":
-                    # fp16 O2 too (reference GradStorage is fp16 there): the
-                    # epilogue's norm partials are then of the stored fp16
-                    # values, so a gradient that overflows 16 bits makes the
-                    # norm non-finite and the loss scaler skips the step
                     g16 = {torch.bfloat16: "bfloat16", torch.float16: "float16"}.get(self._dtype)
-                    gd = g16 if (g16 is not None and self._accumulate_steps == 1
-                                 and not self._pipeline
-                                 and self._sharding_stage == 0) else "float32"
+                    gd = g16 if (g16 is not None and self._sharding_stage == 0) else "float32"
                 gdt = {"float32": torch.float32, "bfloat16": torch.bfloat16,
                        "float16": torch.float16}[gd]
-                if gdt != torch.float32 and self._accumulate_steps > 1:
-                    raise ValueError("Distributed.comm.grad_dtype=%s needs accumulate_steps == 1 "
-                                     "(gradients are written, not accumulated, in 16 bits)" % gd)
+                if gdt != torch.float32 and self._sharding_stage >= 1:
+                    raise ValueError("Distributed.comm.grad_dtype=%s: ZeRO sharding keeps fp32 "
+                                     "gradient shards (use float32 or auto)" % gd)
                 # stage 1 (and stage 2 under pipeline parallelism, where the
                 # tied-embedding reduction needs the flat layout)
                 self.buffer = FlatParamGradBuffer(

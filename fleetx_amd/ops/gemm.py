@@ -465,9 +465,10 @@ def covers_wgrad(dy2, x2):
 def linear_wgrad(dy2, x2, out32, accumulate, sq=None):
     """``out32[N,K] (+)= dy2[M,N]^T @ x2[M,K]`` in fp32.  Returns True if done.
 
-    ``out32`` may also be 16-bit (the bf16 gradient storage of
+    ``out32`` may also be 16-bit (the bf16 / fp16 gradient storage of
     ``Distributed.comm.grad_dtype``): fp32 accumulation, one rounding in the
-    epilogue, never ``accumulate``.
+    epilogue; with ``accumulate`` (micro-batches, pipeline schedules) the
+    stored value joins the fp32 sum before that rounding.
 
     ``sq`` (fp32, :func:`sq_slots` long): the epilogue also writes the sums of
     squares of the values it stores (of the fp32 values for a 16-bit output),
@@ -477,8 +478,7 @@ def linear_wgrad(dy2, x2, out32, accumulate, sq=None):
     if not enabled() or not _ok(dy2, x2) or dy2.dtype != x2.dtype:
         return False
     out16 = out32.dtype == dy2.dtype
-    if (out32.dtype != torch.float32 and not out16) or not out32.is_contiguous() \
-            or (out16 and accumulate):
+    if (out32.dtype != torch.float32 and not out16) or not out32.is_contiguous():
         return False
     M, N = dy2.shape
     K = x2.shape[1]
@@ -488,7 +488,7 @@ def linear_wgrad(dy2, x2, out32, accumulate, sq=None):
     if sq is not None and (sq.dtype != torch.float32 or sq.numel() < sq_slots(N, K)):
         raise ValueError("linear_wgrad: sq needs {} fp32 slots".format(sq_slots(N, K)))
     rc = -1
-    if out16 and N < K and WGRAD_T:
+    if out16 and N < K and WGRAD_T and not accumulate:
         # wide gradient (FC2: [4096, 16384]): run the transposed product
         # x^T dy, the FC1 operand order, and store it transposed.  The FC2 order
         # takes 46 % more L2 misses (profiles/r5_gemm_pmc/); -7 = the shape

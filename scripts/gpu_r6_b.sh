@@ -2,7 +2,7 @@
 # Round 6: new / changed GPU tests first, then the full GPU suite, smoke, FA lab tests
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r6b
+O=gpurun_out/${OUT:-r6b}
 mkdir -p $O
 PT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 timeout -k 10 600 $PT tests/test_fp16_gpu.py "tests/test_multirank_gpu.py::test_tp_oneshot_allreduce_matches_single_rank" "tests/test_multirank_gpu.py::test_zero1_other_optimizers_gather_params" > $O/new.log 2>&1 || { echo "FAIL new"; tail -40 $O/new.log; exit 1; }

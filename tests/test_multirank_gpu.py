@@ -81,7 +81,7 @@ def _train_gpu(rank, world, layout, steps=3, extra=()):
     eng.optimizer.sync_state()
     pf = eng.optimizer.buffer.param_flat
     return {"losses": losses, "gnorms": gnorms, "pnorm": _master_norm(eng), "drank": drank,
-            "pflat": pf.detach().float().cpu(),
+            "pflat": pf.detach().float().cpu(), "gdtype": str(eng.buffer.grad_dtype),
             "native": _lib.kernels() is not None, "master": gather_master_state(eng),
             "master0": master0,
             "overlap": getattr(eng.optimizer, "_overlap_groups", None) is not None}
@@ -197,6 +197,11 @@ LAYOUTS = {
 @pytest.mark.parametrize("name", sorted(LAYOUTS))
 def test_layout_matches_single_rank_on_gpu(ref_gpu, name):
     out = dist_utils.run(_train_gpu, 2, LAYOUTS[name], timeout=300)
+    # 16-bit gradient storage (reduced in 16 bits, averaged first) on every
+    # unsharded layout, micro-batch accumulation and 1F1B included; ZeRO keeps
+    # fp32 gradient shards
+    want = "torch.float32" if LAYOUTS[name][4] >= 1 else "torch.bfloat16"
+    assert all(r["gdtype"] == want for r in out), [r["gdtype"] for r in out]
     _check(out, ref_gpu)
 
 
