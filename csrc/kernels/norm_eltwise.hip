@@ -42,6 +42,20 @@ __device__ __forceinline__ float drop_apply(float v, uint64_t idx, const DropCfg
   return r >= d.thr ? v * d.scale : 0.f;
 }
 
+// The 8 consecutive elements idx0 .. idx0 + 7 of one 16-byte vector (idx0 a
+// multiple of 8 at every call site: row * h + 8-aligned column): one hash per
+// element PAIR, each pair's low / high halves for its even / odd element --
+// the same masks as drop_apply per element, with half the hashing VALU.
+__device__ __forceinline__ void drop_apply8(float* v, uint64_t idx0, const DropCfg& d) {
+  if (!d.enabled) return;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t h = elem_rand_pair(idx0 + 2 * q, d.klo, d.khi);
+    v[2 * q] = (h & 0xffffu) >= d.thr ? v[2 * q] * d.scale : 0.f;
+    v[2 * q + 1] = (h >> 16) >= d.thr ? v[2 * q + 1] * d.scale : 0.f;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Fused forward:  s = residual + dropout(x + bias);  y = LN(s) * g + b
 // Any of residual/bias may be null; dropout optional.  If s_out is null the
@@ -61,6 +75,31 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const size_t base = (size_t)row * h;
+  // Every global load of the row is issued before the first use, each
+  // optional operand under ONE wave-uniform branch around its whole batch: a
+  // per-vector `if (ptr)` around the loads made hipcc wait for each load
+  // before issuing the next (40 loads, 36 waits at h 4096; 3.5 TB/s).
+  uint4 xr[VPT], rr[VPT], br[VPT];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = (i * 64 + lane) * 8;
+    xr[i] = rr[i] = br[i] = make_uint4(0, 0, 0, 0);
+    if (!MASK || c < h) xr[i] = *reinterpret_cast<const uint4*>(x + base + c);
+  }
+  if (residual) {
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      if (!MASK || c < h) rr[i] = *reinterpret_cast<const uint4*>(residual + base + c);
+    }
+  }
+  if (bias) {
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      if (!MASK || c < h) br[i] = *reinterpret_cast<const uint4*>(bias + c);
+    }
+  }
   float v[VPT][8];
   float sum = 0.f;
 #pragma unroll
@@ -71,20 +110,19 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
       for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
       continue;
     }
-    load8<T>(x + base + c, v[i]);
+    unpack8<T>(xr[i], v[i]);
     if (bias) {
       float b[8];
-      load8<T>(bias + c, b);
+      unpack8<T>(br[i], b);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[i][j] += b[j];
     }
     if (drop.enabled) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[i][j] = drop_apply(v[i][j], base + c + j, drop);
+      drop_apply8(v[i], base + c, drop);
     }
     if (residual) {
       float r[8];
-      load8<T>(residual + base + c, r);
+      unpack8<T>(rr[i], r);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[i][j] += r[j];
     }
@@ -149,7 +187,7 @@ __global__ __launch_bounds__(256) void add_ln_fwd_generic(
       for (int j = 0; j < 8; ++j) v[j] += b[j];
     }
     if (drop.enabled)
-      for (int j = 0; j < 8; ++j) v[j] = drop_apply(v[j], base + c + j, drop);
+      drop_apply8(v, base + c, drop);
     if (residual) {
       float r[8];
       load8<T>(residual + base + c, r);
@@ -224,6 +262,17 @@ __global__ __launch_bounds__(256) void ln_bwd_row_kernel(
       s2 += gdy[i][j] * xh[i][j];
     }
   }
+  // ds_in's loads go out before the row reductions, all under one branch (a
+  // per-vector `if (ds_in)` load after them was waited on one by one)
+  uint4 dr[VPT];
+  if (ds_in) {
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      dr[i] = make_uint4(0, 0, 0, 0);
+      if (!MASK || c < h) dr[i] = *reinterpret_cast<const uint4*>(ds_in + base + c);
+    }
+  }
   const float m1 = wave_sum(s1) / h, m2 = wave_sum(s2) / h;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
@@ -234,14 +283,13 @@ __global__ __launch_bounds__(256) void ln_bwd_row_kernel(
     for (int j = 0; j < 8; ++j) o[j] = rstd * (gdy[i][j] - m1 - xh[i][j] * m2);
     if (ds_in) {
       float r[8];
-      load8<T>(ds_in + base + c, r);
+      unpack8<T>(dr[i], r);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] += r[j];
     }
     store8<T>(ds_out + base + c, o);
     if (drop.enabled) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = drop_apply(o[j], base + c + j, drop);
+      drop_apply8(o, base + c, drop);
       store8<T>(dx_out + base + c, o);
     } else if (dx_out != ds_out) {
       store8<T>(dx_out + base + c, o);
@@ -290,7 +338,7 @@ __global__ __launch_bounds__(256) void ln_bwd_row_generic(
     }
     store8<T>(ds_out + base + c, o);
     if (drop.enabled) {
-      for (int j = 0; j < 8; ++j) o[j] = drop_apply(o[j], base + c + j, drop);
+      drop_apply8(o, base + c, drop);
       store8<T>(dx_out + base + c, o);
     } else if (dx_out != ds_out) {
       store8<T>(dx_out + base + c, o);
@@ -416,8 +464,7 @@ __global__ __launch_bounds__(256, 2) void ln_bwd_cols_kernel(
       }
       store8<T>(ds_out + base + c, o);
       if (drop.enabled) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = drop_apply(o[j], base + c + j, drop);
+        drop_apply8(o, base + c, drop);
         store8<T>(dx_out + base + c, o);
       } else if (dx_out != ds_out) {
         store8<T>(dx_out + base + c, o);
@@ -787,8 +834,7 @@ __global__ __launch_bounds__(256) void bias_dropout_add_fwd_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) a[j] += b[j];
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) a[j] = drop_apply(a[j], (uint64_t)off + j, drop);
+    drop_apply8(a, (uint64_t)off, drop);
     if (residual) {
       float r[8];
       load8<T>(residual + off, r);
@@ -822,8 +868,7 @@ __global__ __launch_bounds__(256) void dropout_bwd_colsum_kernel(
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const size_t off = (size_t)(r + 16 * q) * cols + col;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) g[q][j] = drop_apply(g[q][j], off + j, drop);
+        drop_apply8(g[q], off, drop);
         if (dx) {
           store8<T>(dx + off, g[q]);
 #pragma unroll
@@ -837,8 +882,7 @@ __global__ __launch_bounds__(256) void dropout_bwd_colsum_kernel(
       const size_t off = (size_t)r * cols + col;
       float g[8];
       load8<T>(dout + off, g);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = drop_apply(g[j], off + j, drop);
+      drop_apply8(g, off, drop);
       if (dx) {
         store8<T>(dx + off, g);
 #pragma unroll
@@ -871,8 +915,7 @@ __global__ __launch_bounds__(256) void dropout_fwd_kernel(const uint16_t* __rest
     const long off = v * 8;
     float a[8];
     load8<T>(x + off, a);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) a[j] = drop_apply(a[j], (uint64_t)off + j, drop);
+    drop_apply8(a, (uint64_t)off, drop);
     store8<T>(y + off, a);
   }
 }

@@ -423,9 +423,17 @@ class FlatParamGradBuffer:
             if seg is not None:
                 close(seg)
         allc = chunks[True] + chunks[False]
-        addr = torch.tensor([a for a, _ in allc] or [0], dtype=torch.int64, device=self.device)
-        lens = torch.tensor([n for _, n in allc] or [0], dtype=torch.int64, device=self.device)
-        return addr, lens, len(allc), len(chunks[True]), extra
+        # host -> device through PINNED staging kept alive with the plan: a plan
+        # first built inside a HIP-graph capture records the H2D copy, and
+        # every replay re-reads its source (a freed pageable temporary would
+        # feed the replays whatever the allocator put there since)
+        host = torch.tensor([[a for a, _ in allc] or [0], [n for _, n in allc] or [0]],
+                            dtype=torch.int64)
+        if self.device.type == "cuda":
+            host = host.pin_memory()
+        dev = host.to(self.device, non_blocking=True)
+        self._norm_plan_host = getattr(self, "_norm_plan_host", []) + [host]
+        return dev[0], dev[1], len(allc), len(chunks[True]), extra
 
     def _finish_fused_norm(self):
         from ..ops import _lib

@@ -44,6 +44,22 @@ def main():
         ("bias_dropout_add_p0.1", lambda: ops.bias_dropout_add(x, b, r, p=0.1, key=1), 3 * E),
         ("gelu_tanh_16k", lambda: gelu_plain(hh), 2 * 4 * E),
     ]
+    from fleetx_amd.ops import _lib
+    k = _lib.kernels()
+    mean = torch.zeros(M, device="cuda")
+    rstd = torch.ones(M, device="cuda")
+    ds = torch.empty_like(x)
+    dx = torch.empty_like(x)
+
+    def ln_bwd(ds_in, p):
+        k.ln_bwd_row(0, x.data_ptr(), r.data_ptr(), mean.data_ptr(), rstd.data_ptr(), g.data_ptr(),
+                     _lib.ptr(ds_in), ds.data_ptr(), (dx if p > 0 else ds).data_ptr(), M, h,
+                     float(p), 7, _lib.stream())
+    # the row pass of the two-pass LayerNorm backward (h > 2048): dy, s (+ ds_in)
+    # read, ds (+ dropout'd dx) written
+    cases += [("ln_bwd_row_dsin_p0.1", lambda: ln_bwd(x, 0.1),
+               5 * E),
+              ("ln_bwd_row_p0", lambda: ln_bwd(None, 0.0), 3 * E)]
     for name, fn, nbytes in cases:
         ms = timeit(fn)
         print(json.dumps({"kernel": name, "us": round(ms * 1e3, 1),
