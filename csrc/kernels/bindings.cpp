@@ -40,6 +40,7 @@ void fx_ce_bwd(int, const void*, void*, const int64_t*, const float*, const floa
                int, hipStream_t);
 int fx_sumsq_blocks(long n);
 void fx_sumsq_f32(const float*, long, float*, int, hipStream_t);
+void fx_sumsq_16(int, const void*, long, float*, int, hipStream_t);
 void fx_sumsq_chunks(const int64_t*, const int64_t*, int, float*, hipStream_t);
 void fx_adamw_tune(int, int, int);
 void fx_adamw_flat(int, float*, const float*, float*, float*, void*, long, float, float, float,
@@ -221,6 +222,9 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.def("sumsq_f32", [](ptr x, long n, ptr partial, int blocks, ptr st) {
     fx_sumsq_f32(F(x), n, F(partial), blocks, S(st));
+  });
+  m.def("sumsq_16", [](int dt, ptr x, long n, ptr partial, int blocks, ptr st) {
+    fx_sumsq_16(dt, CP(x), n, F(partial), blocks, S(st));
   });
   m.def("adamw_tune", &fx_adamw_tune, py::arg("grid"), py::arg("nt"), py::arg("wide") = 0);
   m.def("adamw_flat", [](int dt, ptr p, ptr g, ptr mm, ptr vv, ptr p16, long n, float lr,

@@ -162,6 +162,34 @@ __global__ __launch_bounds__(256) void sumsq_f32_kernel(const float* __restrict_
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
+// partial[block] = sum of squares of a 16-bit (bf16 / fp16) range, fp32
+// accumulation: the gradient norm over 16-bit gradient storage reads 2 B per
+// element (the torch form `g.float().square().sum()` wrote and re-read an
+// fp32 copy: ~15 ms per 6.7B step); 16-byte loads, a non-finite element
+// (fp16 overflow) makes the sum non-finite
+template <typename T>
+__global__ __launch_bounds__(256) void sumsq_16_kernel(const uint16_t* __restrict__ x, long n,
+                                                       float* __restrict__ partial) {
+  float s = 0.f;
+  const long n8 = (reinterpret_cast<uintptr_t>(x) & 15) == 0 ? n / 8 : 0;
+  const uint4* x8 = reinterpret_cast<const uint4*>(x);
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    float f[8];
+    unpack8<T>(x8[i], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += f[j] * f[j];
+  }
+  for (long i = n8 * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float f = Elt<T>::to_f(x[i]);
+    s += f * f;
+  }
+  __shared__ float red[4];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
 // --------------------------------------------------------------- AdamW
 // p (fp32 master), g (fp32), m, v (fp32); optional 16-bit model copy.
 //  * gscale: device scalar multiplied into g (clip coefficient x 1/loss-scale);
@@ -521,6 +549,11 @@ extern "C" void fx_sumsq_chunks(const int64_t* addr, const int64_t* len, int nch
   if (nchunks > 0) sumsq_chunks_kernel<<<nchunks, 256, 0, st>>>(addr, len, partial);
 }
 
+extern "C" void fx_sumsq_16(int dtype, const void* x, long n, float* partial, int blocks,
+                            hipStream_t st) {
+  FX_DISPATCH_T(dtype, sumsq_16_kernel<T><<<blocks, 256, 0, st>>>(
+                           reinterpret_cast<const uint16_t*>(x), n, partial));
+}
 extern "C" void fx_sumsq_f32(const float* x, long n, float* partial, int blocks, hipStream_t st) {
   sumsq_f32_kernel<<<blocks, 256, 0, st>>>(x, n, partial);
 }

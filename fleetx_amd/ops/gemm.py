@@ -236,9 +236,21 @@ def _dt_name(dtype):
     return "bf16" if dtype == torch.bfloat16 else "fp16"
 
 
+def _plan_entry(kind, dtype, M, N, K):
+    """The plan entry of a shape; fp16 shapes the plan lacks take the bf16
+    entry (same kernels, same MFMA cycle counts, same tile orders: the fp16
+    O2 step otherwise raced the QKV data gradient onto hipBLASLt plus a
+    transpose, +16 ms per 6.7B step, profiles/r6_fp16/)."""
+    plan = load_plan()
+    e = plan.get((kind, _dt_name(dtype), M, N, K))
+    if e is None and dtype == torch.float16:
+        e = plan.get((kind, "bf16", M, N, K))
+    return e
+
+
 def plan_route(kind, M, N, K, dtype):
     """True / False when the plan fixes the route of this shape, else None."""
-    e = load_plan().get((kind, _dt_name(dtype), M, N, K))
+    e = _plan_entry(kind, dtype, M, N, K)
     if e is None or "route" not in e:
         return None
     return e["route"] == "kernel"
@@ -324,7 +336,7 @@ def _planned_fwd_route(a, b):
     r = _FWD_ROUTE.get(key)
     if r is not None:
         return r
-    e = load_plan().get(("fwd", _dt_name(a.dtype), *key[1:4]))
+    e = _plan_entry("fwd", a.dtype, *key[1:4])
     r = False
     if e is not None:
         if "route" in e:

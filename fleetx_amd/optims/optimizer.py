@@ -34,7 +34,14 @@ class ClipGradByNorm(ClipGradByGlobalNorm):
 
 def _sumsq(t):
     if t.dtype != torch.float32:  # 16-bit gradient storage (grad_dtype)
-        return t.float().square().sum()
+        if not t.is_cuda:
+            return t.float().square().sum()
+        k = _lib.kernels()
+        blocks = k.sumsq_blocks(t.numel())
+        part = torch.empty(blocks, device=t.device, dtype=torch.float32)
+        k.sumsq_16(_lib.dt_code(t.dtype), t.data_ptr(), t.numel(), part.data_ptr(), blocks,
+                   _lib.stream())
+        return part.sum()
     if t.is_cuda:
         k = _lib.kernels()
         blocks = k.sumsq_blocks(t.numel())

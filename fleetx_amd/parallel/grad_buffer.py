@@ -450,10 +450,11 @@ class FlatParamGradBuffer:
         zero = torch.zeros((), dtype=torch.float32, device=self.device)
         dist_sq = part[:nd].sum() if nd else zero
         rep_sq = part[nd:nch].sum() if nch > nd else zero
+        from ..optims.optimizer import _sumsq  # 16-bit ranges: read in place
         for t in extra[True]:
-            dist_sq = dist_sq + t.float().square().sum()
+            dist_sq = dist_sq + _sumsq(t)
         for t in extra[False]:
-            rep_sq = rep_sq + t.float().square().sum()
+            rep_sq = rep_sq + _sumsq(t)
         self.early_norm = (dist_sq, rep_sq)
 
     def _data_groups(self):

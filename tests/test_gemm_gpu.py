@@ -406,11 +406,12 @@ def test_persistent_under_memory_pressure(gemm, persist_mode, act):
 
 
 @pytest.mark.parametrize("M,N,K", [(1024, 768, 512), (8192, 1024, 1024), (16448, 1408, 1408),
-                                   (256, 4096, 4096)])
+                                   (256, 4096, 4096), (2048, 1024, 4096)])
 def test_wgrad_16bit_out(gemm, M, N, K):
     """EPI_F32B: the weight gradient written in bf16 from the fp32
     accumulators (16-bit gradient storage), split-K shapes included; the norm
-    partials are the sums of squares of the fp32 values."""
+    partials are the sums of squares of the fp32 values; with accumulate the
+    stored value is added before the rounding."""
     torch.manual_seed(10)
     dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
@@ -424,7 +425,13 @@ def test_wgrad_16bit_out(gemm, M, N, K):
         float((out.float() - ref).abs().max()) <= float(ref.abs().max()) * 2 ** -7
     assert abs(float(sq.double().sum()) - float(ref.double().pow(2).sum())) < \
         1e-4 * float(ref.double().pow(2).sum())
-    assert not gemm.linear_wgrad(dy, x, out, True)  # 16-bit gradients are never accumulated
+    # accumulation (micro-batches / pipeline schedules): the stored gradient
+    # joins the fp32 sum, one rounding per write
+    prev = out.clone()
+    assert gemm.linear_wgrad(dy, x, out, True)
+    want = (prev.float() + ref).to(torch.bfloat16)
+    assert float((out.float() - want.float()).abs().max()) <= \
+        float(want.float().abs().max()) * 2 ** -7
 
 
 # XCD rectangles (gemm5 ``P.xm``, FLEETX_GEMM_XRECT): each XCD's range of tile

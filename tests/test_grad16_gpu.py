@@ -71,3 +71,20 @@ def test_grad16_training_matches_fp32_gradients(graph):
         err = float((m16[k] - m32[k]).norm())
         rel = 0.02 if m32[k].dim() == 2 else 0.5
         assert err <= rel * float(m32[k].norm()) + 1e-4, (k, err, float(m32[k].norm()))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n", [1, 7, 4096 * 8 + 3, 3_000_001])
+def test_sumsq_16_kernel(dtype, n):
+    """The gradient norm over 16-bit gradient storage reads the 16-bit values
+    in place (``optimizer._sumsq``), against an fp64 reference; an fp16 inf
+    (an overflowed gradient) makes the sum non-finite."""
+    from fleetx_amd.optims.optimizer import _sumsq
+    torch.manual_seed(n)
+    x = torch.randn(n + 1, device="cuda").to(dtype)[1:]  # misaligned start included
+    ref = float(x.double().pow(2).sum())
+    got = float(_sumsq(x))
+    assert abs(got - ref) <= 1e-4 * ref + 1e-6, (got, ref)
+    if dtype == torch.float16 and n > 1:
+        x[n // 2] = float("inf")
+        assert not torch.isfinite(_sumsq(x))

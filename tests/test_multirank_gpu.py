@@ -81,7 +81,7 @@ def _train_gpu(rank, world, layout, steps=3, extra=()):
     eng.optimizer.sync_state()
     pf = eng.optimizer.buffer.param_flat
     return {"losses": losses, "gnorms": gnorms, "pnorm": _master_norm(eng), "drank": drank,
-            "pflat": pf.detach().float().cpu(), "gdtype": str(eng.buffer.grad_dtype),
+            "pflat": pf.detach().float().cpu(), "gdtype": str(getattr(eng.buffer, "grad_dtype", torch.float32)),
             "native": _lib.kernels() is not None, "master": gather_master_state(eng),
             "master0": master0,
             "overlap": getattr(eng.optimizer, "_overlap_groups", None) is not None}
@@ -229,16 +229,16 @@ def _train_gpu_oneshot(rank, world, layout):
     return res
 
 
-@pytest.mark.parametrize("name", ["tp2", "tp2_sp", "pp2_tp2", "pp2_tp2_sp"])
+@pytest.mark.parametrize("name", ["tp2", "tp2_sp", "pp2_tp2"])
 def test_tp_oneshot_allreduce_matches_single_rank(ref_gpu, name):
     """With PP x TP the stages reach different collectives (the first stage
     never calls the CE all-reduce, middle stages only the overlapped TP
     paths), so their lazily created communicators differ: the world MAX of
     the one-shot error flag must still run on every rank each step
     (``comm.world_oneshot_possible``), or the ranks that skip it hang the
-    ones that enter it."""
-    layout = dict(LAYOUTS, pp2_tp2=(1, 2, 2, 1, 0, 2, False, 1),
-                  pp2_tp2_sp=(1, 2, 2, 1, 0, 2, True, 1))[name]
+    ones that enter it.  (Sequence parallelism does not compose with the
+    pipeline model: pipeline_model.py rejects it.)"""
+    layout = dict(LAYOUTS, pp2_tp2=(1, 2, 2, 1, 0, 2, False, 1))[name]
     world = layout[0] * layout[1] * layout[2] * layout[3]
     out = dist_utils.run(_train_gpu_oneshot, world, layout, timeout=300)
     assert any(r["oneshot_calls"] > 0 for r in out), [r["oneshot_calls"] for r in out]
