@@ -2,9 +2,9 @@
 # Round 6: 6.7B graph-step kernel profiles (3 steady steps), bf16 and fp16 O2
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r6j
+O=gpurun_out/${OUT:-r6j}
 mkdir -p $O
-for dt in bf16 fp16; do
+for dt in ${DTS:-bf16 fp16}; do
   ov=""; [ $dt = fp16 ] && ov="Engine.mix_precision.dtype=float16"
   FLEETX_BENCH_OVERRIDES=$ov timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/prof_$dt -o run -- python3 bench.py --steps 5 --warmup 5 > $O/prof_$dt.log 2>&1 || { tail -5 $O/prof_$dt.log; exit 1; }
   f=$(find $O/prof_$dt -name "*kernel_trace.csv" | head -1)
