@@ -221,17 +221,16 @@ class EagerEngine(BasicEngine):
                 # without ZeRO sharding; micro-batch accumulation and pipeline
                 # schedules add each micro-batch into the 16-bit storage (one
                 # fp32 add + one rounding per write, as the reference's 16-bit
-                # GradStorage accumulates).  6.7B step on one MI355X: -4.4 ms
+                # GradStorage accumulates); under ZeRO-1 (and stage 2 with a
+                # pipeline, which keeps this flat buffer) the buckets
+                # reduce-scatter in 16 bits.  6.7B step on one MI355X: -4.4 ms
                 # (profiles/r5_grad16/)
                 gd = str(comm.get("grad_dtype", "auto"))
                 if gd == "auto":
                     g16 = {torch.bfloat16: "bfloat16", torch.float16: "float16"}.get(self._dtype)
-                    gd = g16 if (g16 is not None and self._sharding_stage == 0) else "float32"
+                    gd = g16 if g16 is not None else "float32"
                 gdt = {"float32": torch.float32, "bfloat16": torch.bfloat16,
                        "float16": torch.float16}[gd]
-                if gdt != torch.float32 and self._sharding_stage >= 1:
-                    raise ValueError("Distributed.comm.grad_dtype=%s: ZeRO sharding keeps fp32 "
-                                     "gradient shards (use float32 or auto)" % gd)
                 # stage 1 (and stage 2 under pipeline parallelism, where the
                 # tied-embedding reduction needs the flat layout)
                 self.buffer = FlatParamGradBuffer(

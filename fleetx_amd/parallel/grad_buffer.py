@@ -140,10 +140,11 @@ class FlatParamGradBuffer:
         self.reduce_dtype = reduce_dtype
         # 16-bit gradient storage (Distributed.comm.grad_dtype; reference: the
         # O2 GradStorage in the parameter dtype, tensor_fusion_helper.py:56,72-74)
-        # for the GEMM-written weight matrices; unsharded buffers only, and
-        # only in the model dtype (the GEMM epilogue rounds its fp32 tile once)
-        g16 = grad_dtype in (torch.bfloat16, torch.float16) and grad_dtype == self.dtype \
-            and self.shard_stage == 0
+        # for the GEMM-written weight matrices, in the model dtype only (the
+        # GEMM epilogue rounds its fp32 tile once per write); under ZeRO the
+        # buckets reduce-scatter in 16 bits and each rank updates its owned
+        # 16-bit chunk
+        g16 = grad_dtype in (torch.bfloat16, torch.float16) and grad_dtype == self.dtype
         self.grad_dtype = grad_dtype if g16 else torch.float32
 
         cats = {}
@@ -497,7 +498,9 @@ class FlatParamGradBuffer:
             n = self.shard_group.nranks
             r = self.shard_group.rank
             chunk = (b.end - b.start) // n
-            out = self.grad_flat[b.start + r * chunk:b.start + (r + 1) * chunk]
+            # the owned chunk in the storage dtype (16-bit buckets reduce-scatter
+            # in 16 bits, in place, like the fp32 ones)
+            out = self.grad_slice(b.start + r * chunk, b.start + (r + 1) * chunk)
             if _is_gloo(self.shard_group):
                 works.append(dist.all_reduce(src, group=self.shard_group.group, async_op=True))
                 wire = src[r * chunk:(r + 1) * chunk] if low else None

@@ -198,9 +198,9 @@ LAYOUTS = {
 def test_layout_matches_single_rank_on_gpu(ref_gpu, name):
     out = dist_utils.run(_train_gpu, 2, LAYOUTS[name], timeout=300)
     # 16-bit gradient storage (reduced in 16 bits, averaged first) on every
-    # unsharded layout, micro-batch accumulation and 1F1B included; ZeRO keeps
-    # fp32 gradient shards
-    want = "torch.float32" if LAYOUTS[name][4] >= 1 else "torch.bfloat16"
+    # layout with the flat buffer -- micro-batch accumulation, 1F1B and ZeRO-1
+    # included; ZeRO-2/3 keep their own fp32 gradient shards
+    want = "torch.float32" if LAYOUTS[name][4] >= 2 else "torch.bfloat16"
     assert all(r["gdtype"] == want for r in out), [r["gdtype"] for r in out]
     _check(out, ref_gpu)
 
