@@ -406,7 +406,16 @@ __global__ __launch_bounds__(256, 2) void ln_bwd_cols_kernel(
         if (MASK && c >= hw) continue;
         ca[i] = *reinterpret_cast<const uint4*>(s + base + c);
         cd[i] = *reinterpret_cast<const uint4*>(dy + base + c);
-        if (ds_in) cr[i] = *reinterpret_cast<const uint4*>(ds_in + base + c);
+      }
+      // ds_in under ONE branch around its batch (a per-vector `if` around a
+      // load made hipcc wait for each: profiles/r6_norm/)
+      if (ds_in) {
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+          const int c = (i * 64 + lane) * 8;
+          if (MASK && c >= hw) continue;
+          cr[i] = *reinterpret_cast<const uint4*>(ds_in + base + c);
+        }
       }
       mean = mean_in[r];
       rstd = rstd_in[r];
