@@ -65,6 +65,7 @@ void fx_fa_set_dkdv64(int);
 void fx_fa_set_dq64(int);
 void fx_fa_set_dkdv_vreg(int);
 int fx_fa_lab();
+int fx_fa_set_stamps(void*);
 int fx_flash_fwd(int, const void*, const void*, const void*, void*, float*, const long*, const long*,
                  const long*, const long*, const int*, const float*, long, int, int, int, int, int,
                  int, float, float, uint64_t, hipStream_t);
@@ -287,6 +288,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("fa_set_dkdv64", &fx_fa_set_dkdv64);
   m.def("fa_set_dq64", &fx_fa_set_dq64);
   m.def("fa_set_dkdv_vreg", &fx_fa_set_dkdv_vreg);
+  m.def("fa_set_stamps", [](ptr p) { return fx_fa_set_stamps(P(p)); });  // lab builds: fwd stamps
   m.def("fa_lab", &fx_fa_lab);  // 1 in tools/fa_lab builds (lab attention variants)
   m.def("flash_fwd", [](int dt, ptr q, ptr k, ptr v, ptr out, ptr lse, std::vector<long> qs,
                         std::vector<long> ks, std::vector<long> vs, std::vector<long> os,

@@ -193,6 +193,44 @@ __device__ __forceinline__ short cvt16(float x) {
 // row index (within a 32-row C tile) held in register i for lane half h
 __device__ __forceinline__ int crow(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
+// Store one output row per lane pair from a 32x32 accumulator set in the
+// transposed (column = row of the output) layout: lane l and l + 32 hold the
+// two 8-byte halves of every 16 consecutive columns of the row.  One
+// permlane32 swap per register pair gives lane l columns 8k..8k+7 and lane
+// l + 32 columns 8k+8..8k+15 (k even), so the row leaves as whole 16-byte
+// chunks -- half the store instructions and half the partial-line writes of
+// the 8-byte pieces (the store tail of every attention workgroup).  `ok` must
+// agree between lanes l and l + 32 (same row); every lane runs the swaps.
+template <typename T, int D>
+__device__ __forceinline__ void store_row16(uint16_t* rowp, const floatx16 (&acc)[D / 32],
+                                            float scale, int h, int dval, bool row16, bool ok) {
+  auto pk = [&](float x, float y) {
+    return (uint32_t)Elt<T>::from_f(x * scale) | ((uint32_t)Elt<T>::from_f(y * scale) << 16);
+  };
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int k = 0; k < 4; k += 2) {
+      uint32_t a0 = pk(acc[dt][4 * k + 0], acc[dt][4 * k + 1]);
+      uint32_t a1 = pk(acc[dt][4 * k + 2], acc[dt][4 * k + 3]);
+      uint32_t b0 = pk(acc[dt][4 * k + 4], acc[dt][4 * k + 5]);
+      uint32_t b1 = pk(acc[dt][4 * k + 6], acc[dt][4 * k + 7]);
+      const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+      const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+      a0 = r0[0]; b0 = r0[1];
+      a1 = r1[0]; b1 = r1[1];
+      const int d0 = dt * 32 + 8 * k + 8 * h;  // this lane's 8 columns: d0 .. d0 + 7
+      if (ok && d0 < dval) {
+        if (row16 && d0 + 8 <= dval) {
+          *reinterpret_cast<uint4*>(rowp + d0) = make_uint4(a0, a1, b0, b1);
+        } else {  // unaligned rows / a head dim ending mid-chunk: 8-byte halves
+          *reinterpret_cast<uint2*>(rowp + d0) = make_uint2(a0, a1);
+          if (d0 + 4 < dval) *reinterpret_cast<uint2*>(rowp + d0 + 4) = make_uint2(b0, b1);
+        }
+      }
+    }
+}
+
 // 16 zero bytes in global memory: the LDS-DMA source of tile columns past a
 // head dim that is not a tile width (D = 88 on the 96 tile, 40 on 64), so
 // q / k / v need no zero-padded copies.
@@ -308,6 +346,7 @@ struct AttnParams {
   int dval;              // valid head dim (<= the tile's D; columns past it are zero)
   const uint64_t* salt;  // graph mode: per-replay device salt (fx_set_dropout_salt)
   int pair;              // causal forward: two query blocks per workgroup (fa_fwd_kernel)
+  int row16;             // output rows 16-byte aligned (store_row16's 16-byte stores)
 };
 
 // per-(batch, head) dropout hash seed; under graph mode the baked key is
@@ -498,11 +537,39 @@ __device__ __forceinline__ void fwd_tile(const AttnParams& P, const Frag<D>& F, 
 // one block per workgroup in LPT order.)
 __device__ __forceinline__ bool fa_pair_on(const AttnParams& P) { return P.pair != 0; }
 
+#ifdef FX_FA_LAB
+// Lab builds: per-wave s_memrealtime (100 MHz) stamps of the forward (tools/fa_lab/stamp_fwd.py;
+// 64 slots per wave: 0 XCC / HW id, 1 entry, 2 prologue done, 3 + 2 t after
+// tile t's compute, 4 + 2 t after its barrier, 62 before the last finish, 63 end)
+__device__ unsigned long long* fa_stamps = nullptr;
+#define FA_ST(i)                                                        \
+  do {                                                                  \
+    if (stp) {                                                          \
+      const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();       \
+      if (lane == 0 && (i) < 64) stp[(i)] = t_;                         \
+    }                                                                   \
+  } while (0)
+#else
+#define FA_ST(i) \
+  do {           \
+  } while (0)
+#endif
+
 template <typename T, int D, bool CAUSAL, bool DROP, bool KB, int NW>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KV = 64, TB = KV * D * 2, QB = 32 * NW;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+#ifdef FX_FA_LAB
+  unsigned long long* stp = fa_stamps ? fa_stamps + ((long)blockIdx.x * NW + w) * 64 : nullptr;
+  if (stp) {
+    int xcc, hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    if (lane == 0) stp[0] = ((unsigned long long)(xcc & 15) << 32) | (unsigned)hw;
+  }
+#endif
+  FA_ST(1);
   Frag<D> F;
   F.init(lane);
   const int nq = (P.Sq + QB - 1) / QB;
@@ -570,7 +637,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
   auto finish = [&]() {
     const float ltot = lsum + __shfl_xor(lsum, 32, 64);
     const float inv = ltot > 0.f ? (DROP ? P.drop_scale : 1.f) / ltot : 0.f;
-    if (qi < P.Sq) {
+    if constexpr (D == 128) {
+      store_row16<T, D>(P.out + b * P.so_b + hd * P.so_h + (long)qi * P.so_s, oacc, inv, h,
+                        P.dval, P.row16, qi < P.Sq);
+      if (qi < P.Sq && h == 0)
+        P.lse[(long)bh * P.Sq + qi] = ltot > 0.f ? (m_run + log2f(ltot)) * LN2 : INFINITY;
+    } else if (qi < P.Sq) {
+      // D 64 / 96: 8-byte pieces (the swaps' registers would cost these
+      // kernels a wave per SIMD)
       uint16_t* op = P.out + b * P.so_b + hd * P.so_h + (long)qi * P.so_s;
 #pragma unroll
       for (int dt = 0; dt < D / 32; ++dt)
@@ -601,6 +675,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
   }
   glds_wait();
   __syncthreads();
+  FA_ST(2);
 
   short8 qn[D / 16];  // the second item's Q fragments, loaded under the first's last tile
   for (int it = 0; it < ntiles; ++it) {
@@ -614,8 +689,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
       kld.load(row_of(it + 1), smem + (cur ^ 1) * TB, lane);
       vld.load(row_of(it + 1), smem + 2 * TB + (cur ^ 1) * TB, lane);
     }
+#ifdef FA_EXP_NOMASK  // lab timing experiment: the causal grid with the full tile body
+    fwd_tile<T, D, false, DROP, KB>(P, F, kt, vt, qf, oacc, m_run, lsum, row_of(it), wq0, qi,
+                                    kv_len, b, h, sl2, cb);
+#else
     fwd_tile<T, D, CAUSAL, DROP, KB>(P, F, kt, vt, qf, oacc, m_run, lsum, row_of(it), wq0, qi,
                                      kv_len, b, h, sl2, cb);
+#endif
+    FA_ST(3 + 2 * it);
     if (switch_item) {
       finish();
 #pragma unroll
@@ -631,13 +712,16 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_kernel(AttnParams P) {
     }
     glds_wait();
     __syncthreads();
+    FA_ST(4 + 2 * it);
   }
   if (qb2 >= 0 && ntA == 0) {  // kv_len == 0: no tile switched the items; both rows are empty
     finish();
     wq0 = qb2 * QB + w * 32;
     qi = wq0 + (lane & 31);
   }
+  FA_ST(62);
   finish();
+  FA_ST(63);
 }
 
 // ============================================================================
@@ -804,21 +888,8 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_kernel(AttnParams P) {
     glds_wait();
     __syncthreads();
   }
-  if (qvalid) {
-    uint16_t* dqp = P.dq + b * P.sdq_b + hd * P.sdq_h + (long)qi * P.sdq_s;
-#pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        ushort4 o;
-        o.x = Elt<T>::from_f(dqacc[dt][4 * g + 0] * P.scale);
-        o.y = Elt<T>::from_f(dqacc[dt][4 * g + 1] * P.scale);
-        o.z = Elt<T>::from_f(dqacc[dt][4 * g + 2] * P.scale);
-        o.w = Elt<T>::from_f(dqacc[dt][4 * g + 3] * P.scale);
-        if (dt * 32 + 8 * g + 4 * h < P.dval)
-          *reinterpret_cast<ushort4*>(dqp + dt * 32 + 8 * g + 4 * h) = o;
-      }
-  }
+  store_row16<T, D>(P.dq + b * P.sdq_b + hd * P.sdq_h + (long)qi * P.sdq_s, dqacc, P.scale, h,
+                    P.dval, P.row16, qvalid);
 }
 
 
@@ -1083,28 +1154,9 @@ __device__ __forceinline__ void dkdv_body(const AttnParams& P, char* smem) {
     glds_wait();
     __syncthreads();
   }
-  if (ki < P.Sk) {
-    uint16_t* dkp = P.dk + b * P.sdk_b + hd * P.sdk_h + (long)ki * P.sdk_s;
-    uint16_t* dvp = P.dv + b * P.sdk_b + hd * P.sdk_h + (long)ki * P.sdk_s;
-#pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        ushort4 a, c;
-        a.x = Elt<T>::from_f(dkacc[dt][4 * g + 0] * P.scale);
-        a.y = Elt<T>::from_f(dkacc[dt][4 * g + 1] * P.scale);
-        a.z = Elt<T>::from_f(dkacc[dt][4 * g + 2] * P.scale);
-        a.w = Elt<T>::from_f(dkacc[dt][4 * g + 3] * P.scale);
-        c.x = Elt<T>::from_f(dvacc[dt][4 * g + 0]);
-        c.y = Elt<T>::from_f(dvacc[dt][4 * g + 1]);
-        c.z = Elt<T>::from_f(dvacc[dt][4 * g + 2]);
-        c.w = Elt<T>::from_f(dvacc[dt][4 * g + 3]);
-        if (dt * 32 + 8 * g + 4 * h < P.dval)
-          *reinterpret_cast<ushort4*>(dkp + dt * 32 + 8 * g + 4 * h) = a;
-        if (dt * 32 + 8 * g + 4 * h < P.dval)
-          *reinterpret_cast<ushort4*>(dvp + dt * 32 + 8 * g + 4 * h) = c;
-      }
-  }
+  const long krow = b * P.sdk_b + hd * P.sdk_h + (long)ki * P.sdk_s;
+  store_row16<T, D>(P.dk + krow, dkacc, P.scale, h, P.dval, P.row16, ki < P.Sk);
+  store_row16<T, D>(P.dv + krow, dvacc, 1.f, h, P.dval, P.row16, ki < P.Sk);
 }
 
 #ifdef FX_FA_LAB
@@ -1215,7 +1267,11 @@ extern "C" int fx_fa_lab() { return 1; }
 extern "C" void fx_fa_set_dkdv64(int on) { g_dkdv64 = on < 0 ? -1 : (on != 0); }
 extern "C" void fx_fa_set_dkdv_vreg(int on) { g_dkdv_vreg = on < 0 ? -1 : (on != 0); }
 extern "C" void fx_fa_set_dq64(int on) { g_dq64 = on < 0 ? -1 : (on != 0); }
+extern "C" int fx_fa_set_stamps(void* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(fa_stamps), &p, sizeof(p)) == hipSuccess ? 1 : 0;
+}
 #else
+extern "C" int fx_fa_set_stamps(void*) { return 0; }  // production build: no stamps
 extern "C" int fx_fa_lab() { return 0; }  // production build: no lab variants
 extern "C" void fx_fa_set_dkdv64(int) {}
 extern "C" void fx_fa_set_dkdv_vreg(int) {}
@@ -1267,6 +1323,12 @@ static int fwd_waves() {
     else FA_DISPATCH_D(KERNEL, 64, causal, drop, kbias, grid, smem, st, P);             \
   } while (0)
 
+// every output row starts 16-byte aligned (store_row16's 16-byte stores)
+static bool rows16(const void* base, const long* s) {
+  return (reinterpret_cast<uintptr_t>(base) & 15) == 0 && s[0] % 8 == 0 && s[1] % 8 == 0 &&
+         s[2] % 8 == 0;
+}
+
 // strides arrays are {batch, seq, head} in elements; head dim contiguous.
 // kbias: optional [B, kb_stride] float additive key bias; kb_stride must be
 // >= round_up(Sk, 128) (tiles read whole 64-key groups).
@@ -1289,6 +1351,7 @@ static int flash_fwd_t(const void* q, const void* k, const void* v, void* out, f
   P.kbias = kbias;
   P.kb_b = kb_stride;
   P.so_b = os[0]; P.so_s = os[1]; P.so_h = os[2];
+  P.row16 = rows16(out, os);
   const int nw = D == 96 ? waves_for(Sq) : fwd_waves();
   const int nq = (Sq + 32 * nw - 1) / (32 * nw);
   P.pair = causal && fa_pair_grid() ? 1 : 0;
@@ -1334,6 +1397,7 @@ static int flash_bwd_t(const void* q, const void* k, const void* v, const void* 
   P.so_b = os[0]; P.so_s = os[1]; P.so_h = os[2];
   P.sdk_b = dks[0]; P.sdk_s = dks[1]; P.sdk_h = dks[2];
   P.sdq_b = dqs[0]; P.sdq_s = dqs[1]; P.sdq_h = dqs[2];
+  P.row16 = rows16(dq, dqs) && rows16(dk, dks) && rows16(dv, dks);
   const bool drop = p > 0.f, kb = kbias != nullptr;
   {
     const size_t smem = 4 * 64 * D * 2;

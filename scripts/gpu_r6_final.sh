@@ -10,5 +10,5 @@ timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke
 tail -1 $O/smoke.log
 timeout -k 10 300 python3 bench.py > $O/bench.log 2>&1 || { tail -5 $O/bench.log; exit 1; }
 grep '"metric"' $O/bench.log | cut -c1-220
-FLEETX_KERNELS_LIB=$(ls tools/fa_lab/_kernels*.so) timeout -k 10 300 python -u -m pytest tools/fa_lab/test_fa_wave64_lab.py -x -q --timeout 120 --timeout-method thread > $O/fa_lab.log 2>&1 || { tail -20 $O/fa_lab.log; exit 1; }
+FLEETX_KERNELS_LIB=$(ls tools/fa_lab/_kernels.cpython*.so) timeout -k 10 300 python -u -m pytest tools/fa_lab/test_fa_wave64_lab.py -x -q --timeout 120 --timeout-method thread > $O/fa_lab.log 2>&1 || { tail -20 $O/fa_lab.log; exit 1; }
 tail -1 $O/fa_lab.log

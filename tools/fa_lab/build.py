@@ -21,15 +21,18 @@ def main():
     B.build_kernels()  # production objects up to date
     kdir = os.path.join(B.CSRC, "kernels")
     inc = os.path.join(HERE, "fa_wave64.inc")
-    obj = os.path.join(HERE, "flash_attn_lab.o")
+    # FX_FA_LAB_DEFS="-DNAME ...": an experiment build, named after its defines
+    defs = os.environ.get("FX_FA_LAB_DEFS", "").split()
+    tag = "".join("_" + d[2:].lower() for d in defs)
+    obj = os.path.join(HERE, "flash_attn_lab%s.o" % tag)
     src = os.path.join(kdir, "flash_attn.hip")
     if B._newer(obj, [src, inc]):
         B._run([B.hipcc(), "-O3", "-std=c++17", "-fPIC", "--offload-arch=" + B.ARCH,
-                "-munsafe-fp-atomics", "-Wno-unused-result", '-DFX_FA_LAB="%s"' % inc,
-                "-c", src, "-o", obj])
+                "-munsafe-fp-atomics", "-Wno-unused-result", '-DFX_FA_LAB="%s"' % inc]
+               + defs + ["-c", src, "-o", obj])
     objs = [os.path.join(B.OBJ, f) for f in sorted(os.listdir(B.OBJ))
             if f.endswith(".o") and f != "flash_attn.hip.o"] + [obj]
-    so = os.path.join(HERE, "_kernels" + B.EXT)
+    so = os.path.join(HERE, "_kernels" + tag + B.EXT)
     B._run([B.hipcc(), "-shared", "-fPIC", "--offload-arch=" + B.ARCH, "-o", so] + objs)
     print(so)
 
