@@ -542,16 +542,23 @@ __device__ __forceinline__ bool fa_pair_on(const AttnParams& P) { return P.pair 
 // 64 slots per wave: 0 XCC / HW id, 1 entry, 2 prologue done, 3 + 2 t after
 // tile t's compute, 4 + 2 t after its barrier, 62 before the last finish, 63 end)
 __device__ unsigned long long* fa_stamps = nullptr;
-#define FA_ST(i)                                                        \
+#define FA_STN(i, n)                                                    \
   do {                                                                  \
     if (stp) {                                                          \
-      const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();       \
-      if (lane == 0 && (i) < 64) stp[(i)] = t_;                         \
+      const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();   \
+      if (lane == 0 && (i) < (n)) stp[(i)] = t_;                        \
     }                                                                   \
   } while (0)
+#define FA_ST(i) FA_STN(i, 64)
+// dK/dV pass: 128 slots per wave (slot 0 = key block; tile t at 3 + 2 t /
+// 4 + 2 t, 126 before the dK / dV stores, 127 end; tools/fa_lab/stamp_bwd.py)
+#define FA_ST2(i) FA_STN(i, 128)
 #else
 #define FA_ST(i) \
   do {           \
+  } while (0)
+#define FA_ST2(i) \
+  do {            \
   } while (0)
 #endif
 
@@ -1001,6 +1008,11 @@ __device__ __forceinline__ void dkdv_body(const AttnParams& P, char* smem) {
       c[QT + tid] = nd;
     }
   };
+#ifdef FX_FA_LAB
+  unsigned long long* stp = fa_stamps ? fa_stamps + ((long)blockIdx.x * NW + w) * 128 : nullptr;
+  if (stp && lane == 0) stp[0] = (unsigned long long)kblock;
+#endif
+  FA_ST2(1);
   GldsStream<D, QT, NW> qld, gld;
   qld.init(qp, P.sq_s, P.Sq, w, lane, P.dval);
   gld.init(dop, P.so_s, P.Sq, w, lane, P.dval);
@@ -1012,6 +1024,7 @@ __device__ __forceinline__ void dkdv_body(const AttnParams& P, char* smem) {
   }
   glds_wait();
   __syncthreads();
+  FA_ST2(2);
 
   for (int it = 0; it < ntiles; ++it) {
     const int qb = q_begin + it * QT;
@@ -1150,13 +1163,17 @@ __device__ __forceinline__ void dkdv_body(const AttnParams& P, char* smem) {
         }
       }
     }
+    FA_ST2(3 + 2 * it);
     if (more) rowconst_store(nxt);
     glds_wait();
     __syncthreads();
+    FA_ST2(4 + 2 * it);
   }
+  FA_ST2(126);
   const long krow = b * P.sdk_b + hd * P.sdk_h + (long)ki * P.sdk_s;
   store_row16<T, D>(P.dk + krow, dkacc, P.scale, h, P.dval, P.row16, ki < P.Sk);
   store_row16<T, D>(P.dv + krow, dvacc, 1.f, h, P.dval, P.row16, ki < P.Sk);
+  FA_ST2(127);
 }
 
 #ifdef FX_FA_LAB
