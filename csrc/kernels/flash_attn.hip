@@ -1340,8 +1340,11 @@ static int fwd_waves() {
     else FA_DISPATCH_D(KERNEL, 64, causal, drop, kbias, grid, smem, st, P);             \
   } while (0)
 
-// every output row starts 16-byte aligned (store_row16's 16-byte stores)
+// every output row starts 16-byte aligned (store_row16's 16-byte stores);
+// FLEETX_FA_ROW16=0 forces the 8-byte fallback (tests/test_kernels_gpu.py)
 static bool rows16(const void* base, const long* s) {
+  const char* e = getenv("FLEETX_FA_ROW16");
+  if (e && atoi(e) == 0) return false;
   return (reinterpret_cast<uintptr_t>(base) & 15) == 0 && s[0] % 8 == 0 && s[1] % 8 == 0 &&
          s[2] % 8 == 0;
 }

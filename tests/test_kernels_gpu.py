@@ -199,6 +199,32 @@ def test_flash_attention(D, causal, p):
             qkv.grad[:, :, :, i], ref_in.grad[:, :, :, i]))
 
 
+@pytest.mark.parametrize("D", [128, 40])
+def test_flash_attention_row_store_fallback(D, monkeypatch):
+    """store_row16 writes whole 16-byte row chunks after the lane-pair swap;
+    rows that are not 16-byte aligned take 8-byte halves of the same swapped
+    registers (FLEETX_FA_ROW16=0 forces that path): bitwise the same O, dQ,
+    dK, dV."""
+    from fleetx_amd import ops
+    B, S, H = 2, 300, 4
+    torch.manual_seed(0)
+    qkv0 = (0.5 * torch.randn(B, S, H, 3, D, device=DEV)).bfloat16()
+    g = torch.randn(B, S, H, D, device=DEV).bfloat16()
+
+    def run():
+        qkv = qkv0.clone().requires_grad_()
+        out = ops.flash_attention_qkvpacked(qkv, causal=True, dropout_p=0.1, key=77)
+        out.backward(g)
+        return out.detach(), qkv.grad
+    o16, g16 = run()
+    monkeypatch.setenv("FLEETX_FA_ROW16", "0")
+    o8, g8 = run()
+    monkeypatch.delenv("FLEETX_FA_ROW16")
+    torch.cuda.synchronize()
+    assert torch.equal(o16, o8)
+    assert torch.equal(g16, g8)
+
+
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attention_rescale_branch(causal):
     """Deferred online-softmax rescale (FA_RESCALE_THR = 8, log2 units): one key
