@@ -309,13 +309,11 @@ class EagerEngine(BasicEngine):
                     and hasattr(self.buffer, "enable_early_norm"):
                 self.buffer.enable_early_norm()
             # otherwise the weight-gradient GEMMs hand the norm their sums of
-            # squares (no second pass over the fp32 gradient at step end).
-            # Not under the fp16 loss scaler: replayed in the whole-step graph
-            # after an overflowed (skipped) step, the epilogue partials gave a
-            # norm that differs from the direct pass and from the eager step
-            # (tests/test_fp16_gpu.py); the scaled run takes the direct norm
-            # pass over the 16-bit gradients instead
-            elif comm.get("fused_grad_norm", self.scaler is None) \
+            # squares (no second pass over the gradient at step end); under the
+            # fp16 loss scaler the partials are of the stored fp16 values, so
+            # an overflow makes the norm non-finite (tests/test_fp16_gpu.py:
+            # graph replay bitwise the eager step across an overflowed step)
+            elif comm.get("fused_grad_norm", True) \
                     and hasattr(self.buffer, "enable_fused_norm") \
                     and getattr(self.optimizer, "grad_clip", None) is not None:
                 self.buffer.enable_fused_norm()
