@@ -2,7 +2,7 @@
 # Round 6 end, last tree: full GPU suite, smoke, driver-K/W bench
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r6final3
+O=gpurun_out/r6final4
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
