@@ -7,6 +7,12 @@ the production ``fleetx_amd/_C/_kernels*.so`` does not contain them.
     python tools/fa_lab/build.py            # -> tools/fa_lab/_kernels<EXT>
     FLEETX_KERNELS_LIB=tools/fa_lab/_kernels<EXT> FLEETX_FA_DKDV64=1 python ...
 
+The lab library also carries per-wave ``s_memrealtime`` stamps of the forward
+and dK/dV passes (``fa_set_stamps``; read by ``stamp_fwd.py`` /
+``stamp_bwd.py``).  ``FX_FA_LAB_DEFS="-DNAME ..."`` builds an experiment
+variant named after its defines (e.g. ``-DFA_EXP_NOMASK``: the causal forward
+grid with the full tile body, timing only).
+
 Every other object is the production build's (``build/obj``)."""
 import os
 import sys
